@@ -1,0 +1,99 @@
+"""ctypes binding of libavt.so (the C-ABI declared in include/avt.h) and its build recipe.
+
+The library is built in-tree (``audio-visual-tubes_amd/libavt.so``) with
+``hipcc --offload-arch=gfx950``; it travels to the GPU box with the repo snapshot.  There is no
+CPU fallback: every op raises if the library or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libavt.so")
+SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip"]
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_longlong
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "avt_last_error": (ctypes.c_char_p, []),
+    "avt_abi_version": (_I, []),
+    "avt_conv2d_fwd_stat_tiles": (_I, [_I, _I, _I]),
+    "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_bn_finalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
+    "avt_bn_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P]),
+    "avt_bn_bwd_parts": (_I, [_L, _I]),
+    "avt_bn_bwd_workspace": (_Z, [_L, _I]),
+    "avt_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_maxpool3s2_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "avt_maxpool3s2_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "avt_audio_pool_norm_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    "avt_audio_pool_norm_bwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
+    "avt_hardway_save_floats": (_Z, [_I]),
+    "avt_hardway_fwd": (_I, [_P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "avt_hardway_ce": (_I, [_P, _I, _I, _F, _P, _P, _P]),
+    "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
+    "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "avt_nchw_to_nhwc_bf16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "avt_nhwc_bf16_to_nchw": (_I, [_P, _P, _I, _I, _I, _P]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    """Compile csrc/*.hip for gfx950 into libavt.so (in-tree)."""
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    if not force and os.path.exists(LIB_PATH):
+        newest = max(os.path.getmtime(s) for s in srcs + [os.path.join(CSRC, "avt_common.h")])
+        if os.path.getmtime(LIB_PATH) >= newest:
+            return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp"
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", tmp] + srcs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libavt.so not built ({LIB_PATH}); run __graft_entry__.build()")
+            h = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().avt_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def query(name: str, *args):
+    return getattr(lib(), name)(*args)

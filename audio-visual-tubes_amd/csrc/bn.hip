@@ -1,0 +1,295 @@
+// Train-mode BatchNorm2d (+ReLU, +residual) for the ResNet-18 trunks, NHWC bf16 activations,
+// fp32 statistics.  Semantics of torch BatchNorm2d as used at models/base_models.py:39,46-49,
+// 120-121,141 (eps 1e-5, momentum 0.1): normalise with the biased batch variance, update
+// running_var with the unbiased one.
+//
+//   fwd : stats come from the conv epilogue as per-128-row tile partials (sum, M2 about the tile
+//         mean) -> bn_finalize (Chan merge) -> scale/shift -> bn_apply (+residual, +ReLU).
+//   bwd : bn_bwd_reduce (sum g', sum g'*xhat per block, g' = g*[y>0]) -> bn_bwd_finalize
+//         (dgamma, dbeta, k1, k2) -> bn_bwd_apply: g_c = gamma*invstd*(g' - k1 - xhat*k2).
+#include "avt_common.h"
+
+namespace avt {
+
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+  const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = bf2f(u[e] & 0xffff);
+    f[2 * e + 1] = bf2f(u[e] >> 16);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+  v.x = pack2(f[0], f[1]);
+  v.y = pack2(f[2], f[3]);
+  v.z = pack2(f[4], f[5]);
+  v.w = pack2(f[6], f[7]);
+  return v;
+}
+
+// Chan et al. parallel merge of (n, mean, M2)
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
+  if (nb <= 0.f) return;
+  const float nn = n + nb;
+  const float d = meanb - mean;
+  const float f = nb / nn;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = nn;
+}
+
+// one block = 64 channels x 16 tile-rows (1024 threads)
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float2* __restrict__ part, int ntiles, int rows,
+                                                           int tile_rows, int C, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* running_mean,
+                                                           float* running_var, float momentum, float eps,
+                                                           float* scale, float* shift, float* save_mean,
+                                                           float* save_invstd) {
+  __shared__ float sn[16][64], sm[16][64], s2[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  if (c < C) {
+    for (int t = ty; t < ntiles; t += 16) {
+      const float2 pr = part[(size_t)t * C + c];
+      const float nt = (float)min(tile_rows, rows - t * tile_rows);
+      chan_merge(n, mean, m2, nt, pr.x / nt, pr.y);
+    }
+  }
+  sn[ty][tx] = n;
+  sm[ty][tx] = mean;
+  s2[ty][tx] = m2;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) chan_merge(n, mean, m2, sn[k][tx], sm[k][tx], s2[k][tx]);
+    const float var = m2 / n;
+    const float inv = rsqrtf(var + eps);
+    const float sc = gamma[c] * inv;
+    scale[c] = sc;
+    shift[c] = beta[c] - mean * sc;
+    if (save_mean) save_mean[c] = mean;
+    if (save_invstd) save_invstd[c] = inv;
+    if (running_mean) {
+      const float unb = n > 1.f ? m2 / (n - 1.f) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+  }
+}
+
+// out = [relu]( x*scale + shift + [residual*rscale + rshift | residual] )
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const bf16_t* __restrict__ res, const float* __restrict__ rscale,
+                                                       const float* __restrict__ rshift, bf16_t* __restrict__ out,
+                                                       long long nvec, int C, int relu) {
+  const int cv = C / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * 8;
+    float f[8];
+    unpack8(reinterpret_cast<const u32x4*>(x)[i], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = f[e] * scale[c0 + e] + shift[c0 + e];
+    if (res) {
+      float r[8];
+      unpack8(reinterpret_cast<const u32x4*>(res)[i], r);
+      if (rscale) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e] * rscale[c0 + e] + rshift[c0 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += r[e];
+      }
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+    }
+    reinterpret_cast<u32x4*>(out)[i] = pack8(f);
+  }
+}
+
+// Per-block partial sums of g' and g'*xhat.  Block: 256 threads; thread owns channel chunk
+// (tid % (C/8)) and walks rows tid/(C/8) + k*(256/(C/8)) of the block's row range.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                                            const bf16_t* __restrict__ xc, const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float2* __restrict__ part,
+                                                            int rows, int C, int rows_per_block) {
+  extern __shared__ float red[];  // [256/(C/8)][C][2]
+  const int cv = C / 8;
+  const int chunk = threadIdx.x % cv, r0 = threadIdx.x / cv, rstep = 256 / cv;
+  const int c0 = chunk * 8;
+  float mu[8], is[8], s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[c0 + e];
+    is[e] = invstd[c0 + e];
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+  }
+  const int rbeg = blockIdx.x * rows_per_block, rend = min(rows, rbeg + rows_per_block);
+  if (r0 < rstep) {
+    for (int r = rbeg + r0; r < rend; r += rstep) {
+      const size_t off = (size_t)r * cv + chunk;
+      float gg[8], xx[8];
+      unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
+      unpack8(reinterpret_cast<const u32x4*>(xc)[off], xx);
+      if (y) {
+        float yy[8];
+        unpack8(reinterpret_cast<const u32x4*>(y)[off], yy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += gg[e];
+        s2[e] += gg[e] * (xx[e] - mu[e]) * is[e];
+      }
+    }
+  }
+  const int nr = rstep;  // rows of partials in LDS
+  if (r0 < nr) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * C + c0 + e) * 2] = s1[e];
+      red[(r0 * C + c0 + e) * 2 + 1] = s2[e];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < nr; ++k) {
+      a += red[(k * C + c) * 2];
+      b += red[(k * C + c) * 2 + 1];
+    }
+    part[(size_t)blockIdx.x * C + c] = make_float2(a, b);
+  }
+}
+
+// Sum block partials; write dgamma/dbeta (accumulated into grads if non-null) and k1,k2.
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nparts, int C,
+                                                               float inv_rows, float* dgamma, float* dbeta, float* k1,
+                                                               float* k2) {
+  __shared__ float sa[16][64], sb[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float a = 0.f, b = 0.f;
+  if (c < C)
+    for (int t = ty; t < nparts; t += 16) {
+      const float2 pr = part[(size_t)t * C + c];
+      a += pr.x;
+      b += pr.y;
+    }
+  sa[ty][tx] = a;
+  sb[ty][tx] = b;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    for (int k = 1; k < 16; ++k) {
+      a += sa[k][tx];
+      b += sb[k][tx];
+    }
+    if (dbeta) dbeta[c] += a;
+    if (dgamma) dgamma[c] += b;
+    k1[c] = a * inv_rows;
+    k2[c] = b * inv_rows;
+  }
+}
+
+// g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ xc, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma, const float* __restrict__ k1,
+                                                           const float* __restrict__ k2, bf16_t* __restrict__ gc,
+                                                           bf16_t* __restrict__ gmask_out, long long nvec, int C) {
+  const int cv = C / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % cv) * 8;
+    float gg[8], xx[8], o[8];
+    unpack8(reinterpret_cast<const u32x4*>(g)[i], gg);
+    unpack8(reinterpret_cast<const u32x4*>(xc)[i], xx);
+    if (y) {
+      float yy[8];
+      unpack8(reinterpret_cast<const u32x4*>(y)[i], yy);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float xh = (xx[e] - mean[c]) * invstd[c];
+      o[e] = gamma[c] * invstd[c] * (gg[e] - k1[c] - xh * k2[c]);
+    }
+    reinterpret_cast<u32x4*>(gc)[i] = pack8(o);
+    if (gmask_out) reinterpret_cast<u32x4*>(gmask_out)[i] = pack8(gg);
+  }
+}
+
+static int ew_grid(long long nvec) {
+  long long b = (nvec + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace avt
+
+using namespace avt;
+
+extern "C" int avt_bn_finalize(const void* partial, int ntiles, int rows, int tile_rows, int C, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                               float* scale, float* shift, float* save_mean, float* save_invstd, void* stream) {
+  AVT_REQUIRE(partial && gamma && beta && scale && shift, "bn_finalize: null pointer");
+  AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream,
+                     (const float2*)partial, ntiles, rows, tile_rows, C, gamma, beta, running_mean, running_var,
+                     momentum, eps, scale, shift, save_mean, save_invstd);
+  return check_launch("bn_finalize");
+}
+
+extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual,
+                            const float* rscale, const float* rshift, void* out, long long rows, int C, int relu,
+                            void* stream) {
+  AVT_REQUIRE(x && scale && shift && out, "bn_apply: null pointer");
+  AVT_REQUIRE(C % 8 == 0, "bn_apply: C=%d must be a multiple of 8", C);
+  AVT_REQUIRE((rscale == nullptr) == (rshift == nullptr), "bn_apply: rscale/rshift must be both set or both null");
+  const long long nvec = rows * C / 8;
+  if (nvec == 0) return AVT_OK;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     scale, shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
+  return check_launch("bn_apply");
+}
+
+extern "C" int avt_bn_bwd_parts(long long rows, int C) {
+  const int rows_per_block = 256;
+  return (int)((rows + rows_per_block - 1) / rows_per_block);
+}
+
+extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
+                          const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out,
+                          void* workspace, long long rows, int C, void* stream) {
+  // workspace: avt_bn_bwd_parts(rows,C)*C float2 + 2*C floats
+  AVT_REQUIRE(g && xc && mean && invstd && gamma && gc && workspace, "bn_bwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn_bwd: C=%d unsupported", C);
+  AVT_REQUIRE(rows > 0, "bn_bwd: empty input");
+  const int rpb = 256;
+  const int nparts = avt_bn_bwd_parts(rows, C);
+  float2* part = (float2*)workspace;
+  float* k1 = (float*)(part + (size_t)nparts * C);
+  float* k2 = k1 + C;
+  hipStream_t st = (hipStream_t)stream;
+  const int nr = 256 / (C / 8);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), nr * C * 2 * sizeof(float), st, (const bf16_t*)g,
+                     (const bf16_t*)y, (const bf16_t*)xc, mean, invstd, part, (int)rows, C, rpb);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, nparts, C,
+                     1.0f / (float)rows, dgamma, dbeta, k1, k2);
+  const long long nvec = rows * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
+                     (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc, (bf16_t*)gmask_out, nvec, C);
+  return check_launch("bn_bwd");
+}
+
+extern "C" size_t avt_bn_bwd_workspace(long long rows, int C) {
+  return (size_t)avt_bn_bwd_parts(rows, C) * C * sizeof(float) * 2 + 2 * (size_t)C * sizeof(float);
+}

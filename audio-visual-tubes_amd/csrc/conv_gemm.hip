@@ -1,0 +1,572 @@
+// Implicit-GEMM convolution for the ResNet-18 trunks (fwd, dgrad, wgrad) on gfx950 MFMA.
+//
+// Replaces the implicit cuDNN/MKLDNN Conv2d of models/base_models.py:23-30 (conv3x3/conv1x1),
+// :135-138 (7x7/s2 stems) as called from BasicBlock.forward (:53-69) and _forward_impl (:195-210).
+//
+// Layout: activations NHWC bf16; weights packed bf16.  fp32 accumulate in MFMA AGPRs.
+//   fwd   : C[m = (n,p,q)][k_out]      = sum_{(r,s,c)}  X[n, p*st-pad+r, q*st-pad+s, c] * W[k_out][(r,s,c)]
+//   dgrad : C[m = (n,h,w)][c]          = sum_{(r,s,k)}  DY[n, (h+pad-r)/st, (w+pad-s)/st, k] * WT[c][(r,s,k)]
+//   wgrad : DW[k_out][(r,s,c)]        += sum_{(n,p,q)}  DY[(n,p,q)][k_out] * X[n, p*st-pad+r, q*st-pad+s, c]
+// fwd/dgrad ("NT"): both operands K-contiguous in LDS, fragments by ds_read_b128 (XOR-swizzled rows).
+// wgrad ("TN"): both operands pixel-major in LDS, fragments by ds_read_b64_tr_b16 (hardware transpose).
+// MFMA: v_mfma_f32_32x32x16_bf16, 4 waves (2x2) per 256-thread block, register-staged double buffer.
+#include "avt_common.h"
+
+namespace avt {
+
+// ------------------------------------------------------------------------------------------------
+// NT kernel (fwd / dgrad)
+// ------------------------------------------------------------------------------------------------
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+
+struct GemmNTParams {
+  const bf16_t* act;   // gather source: x [N][IH][IW][IC] (fwd) or dy [N][IH][IW][IC] (dgrad)
+  const bf16_t* wmat;  // [Ng][Kg] bf16, K contiguous
+  bf16_t* out;         // [M][Ng] bf16
+  const bf16_t* add;   // optional [M][Ng] bf16 added to the result (may alias out)
+  float2* stats;       // optional [ceil(M/BM)][Ng] (sum, M2 about the tile mean) of fp32 results
+  int M, Ng, Kg;
+  int IH, IW, IC;      // source tensor geometry
+  int OH, OW;          // pixel grid of the GEMM rows
+  int R, S, stride, pad;
+};
+
+__device__ __forceinline__ int swz64(int row, int chunk) {  // byte offset in a [rows][32 bf16] tile
+  return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+}
+
+template <int MODE, int CVEC, int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 tiles per wave (waves 2x2)
+  constexpr int AR = BM / 64, BR = BN / 64;  // staged rows per thread
+  constexpr int STAGE_BYTES = 2 * (BM + BN) * 64;
+  constexpr int CT_LD = BN + 8;  // epilogue tile row (bf16 elements)
+  constexpr int EPI_BYTES = BM * CT_LD * 2;
+  constexpr int SMEM = (STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 4 * BN * 4];
+  float* red = reinterpret_cast<float*>(smem + SMEM);  // [2][2][BN] stats scratch
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nnt = p.Ng / BN;
+  const int mt = blockIdx.x / nnt, nt = blockIdx.x % nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  // ---- per-thread load assignment: chunk (tid&3) of rows (tid>>2) + 64*i ----
+  const int lchunk = tid & 3, lrow = tid >> 2;
+  int a_pix[AR], a_y[AR], a_x[AR];
+  bool a_ok[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + lrow + 64 * i;
+    a_ok[i] = m < p.M;
+    const int mm = a_ok[i] ? m : 0;
+    const int hw = p.OH * p.OW;
+    const int n = mm / hw, rem = mm - n * hw;
+    const int oh = rem / p.OW, ow = rem - oh * p.OW;
+    a_pix[i] = n * p.IH * p.IW;
+    if (MODE == MODE_FWD) {
+      a_y[i] = oh * p.stride - p.pad;
+      a_x[i] = ow * p.stride - p.pad;
+    } else {
+      a_y[i] = oh + p.pad;
+      a_x[i] = ow + p.pad;
+    }
+  }
+  const bf16_t* bptr[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) bptr[i] = p.wmat + (size_t)(n0 + lrow + 64 * i) * p.Kg + lchunk * 8;
+
+  u32x4 ra[AR], rb[BR];
+  const int nkt = p.Kg / 32;
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * 32;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const u32x4*>(bptr[i] + k0);
+    if (CVEC == 8) {
+      const int rs = k0 / p.IC, c0 = k0 - rs * p.IC;
+      const int r = rs / p.S, s = rs - r * p.S;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        int y, x;
+        bool ok = a_ok[i];
+        if (MODE == MODE_FWD) {
+          y = a_y[i] + r;
+          x = a_x[i] + s;
+        } else {
+          int yn = a_y[i] - r, xn = a_x[i] - s;
+          if (p.stride == 2) {
+            ok = ok && ((yn & 1) == 0) && ((xn & 1) == 0);
+            yn >>= 1;
+            xn >>= 1;
+          }
+          y = yn;
+          x = xn;
+        }
+        ok = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (ok) v = *reinterpret_cast<const u32x4*>(p.act + (size_t)(a_pix[i] + y * p.IW + x) * p.IC + c0 + lchunk * 8);
+        ra[i] = v;
+      }
+    } else {
+      // stems: C == CVEC (1 or 4), k = (r*S + s)*C + c; positions beyond R*S are zero padding
+      const int kc = k0 + lchunk * 8;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        unsigned short e[8];
+#pragma unroll
+        for (int g = 0; g < 8 / CVEC; ++g) {
+          const int pos = (kc + g * CVEC) / CVEC;
+          const int r = pos / p.S, s = pos - r * p.S;
+          const int y = a_y[i] + r, x = a_x[i] + s;
+          const bool ok = a_ok[i] && pos < p.R * p.S && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
+          const bf16_t* src = p.act + (size_t)(a_pix[i] + y * p.IW + x) * CVEC;
+          if (CVEC == 4) {
+            u32x2 v = {0u, 0u};
+            if (ok) v = *reinterpret_cast<const u32x2*>(src);
+            e[g * 4 + 0] = v.x & 0xffff;
+            e[g * 4 + 1] = v.x >> 16;
+            e[g * 4 + 2] = v.y & 0xffff;
+            e[g * 4 + 3] = v.y >> 16;
+          } else {
+            e[g] = ok ? src[0] : (unsigned short)0;
+          }
+        }
+        u32x4 v;
+        v.x = e[0] | ((unsigned)e[1] << 16);
+        v.y = e[2] | ((unsigned)e[3] << 16);
+        v.z = e[4] | ((unsigned)e[5] << 16);
+        v.w = e[6] | ((unsigned)e[7] << 16);
+        ra[i] = v;
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* As = smem + buf * (BM + BN) * 64;
+    char* Bs = As + BM * 64;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) *reinterpret_cast<u32x4*>(As + swz64(lrow + 64 * i, lchunk)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i) *reinterpret_cast<u32x4*>(Bs + swz64(lrow + 64 * i, lchunk)) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int frow = lane & 31, fhalf = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) load_tile(kt + 1);
+    const char* As = smem + cur * (BM + BN) * 64;
+    const char* Bs = As + BM * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / 2) + i * 32 + frow;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + swz64(row, ks * 2 + fhalf));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(row, ks * 2 + fhalf));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: BN partial statistics over valid rows (fp32, before rounding) ----
+  const int rows_valid = min(BM, p.M - m0);
+  if (MODE == MODE_FWD && p.stats != nullptr) {
+    float colsum[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / 2) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          if (r < rows_valid) s += acc[i][j][v];
+        }
+      s += __shfl_xor(s, 32, 64);
+      colsum[j] = s;
+      if (lane < 32) red[wm * BN + wn * (BN / 2) + j * 32 + lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = wn * (BN / 2) + j * 32 + frow;
+      const float mean = (red[c] + red[BN + c]) / (float)rows_valid;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / 2) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          const float d = acc[i][j][v] - mean;
+          if (r < rows_valid) q += d * d;
+        }
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 32) red[2 * BN + wm * BN + c] = q;
+      (void)colsum;
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      p.stats[(size_t)mt * p.Ng + n0 + c] = make_float2(red[c] + red[BN + c], red[2 * BN + c] + red[3 * BN + c]);
+    }
+  }
+
+  // ---- epilogue: bf16 tile through LDS, 16-byte coalesced stores ----
+  bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int r = wm * (BM / 2) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        const int c = wn * (BN / 2) + j * 32 + frow;
+        Ct[r * CT_LD + c] = f2bf(acc[i][j][v]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-byte chunks per row
+  for (int idx = tid; idx < BM * CPR; idx += 256) {
+    const int r = idx / CPR, cc = idx - r * CPR;
+    if (r >= rows_valid) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
+    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
+    if (p.add != nullptr) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+      unsigned* vv = reinterpret_cast<unsigned*>(&v);
+      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
+        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
+        vv[e] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(p.out + off) = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// TN kernel (wgrad): DW[k_out][col] += sum_pix DY[pix][k_out] * X(pix, col)
+// ------------------------------------------------------------------------------------------------
+struct GemmTNParams {
+  const bf16_t* dy;  // [Kred][Mg]
+  const bf16_t* x;   // [N][H][W][Cp]
+  float* dw;         // [Mg][R*S*Creal] fp32 (atomic accumulate)
+  int Mg, Ng, Kred;  // Ng = padded patch width (multiple of BN)
+  int H, W, Cp, Creal, P, Q, R, S, stride, pad;
+  int kt_per_split;
+};
+
+template <int CVEC, int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int ALD = BM + 32, BLD = BN + 32;  // row strides (elements): +64 B keeps tr reads conflict-free
+  constexpr int ACPR = BM / 8, BCPR = BN / 8;  // 16-B chunks per pixel row
+  constexpr int AROWS = 32 * ACPR / 256, BROWS = 32 * BCPR / 256;  // rows staged per thread
+  constexpr int ASTEP = 256 / ACPR, BSTEP = 256 / BCPR;
+  constexpr int BUF = 32 * (ALD + BLD);  // elements per buffer
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nnt = p.Ng / BN;
+  const int mt = blockIdx.x / nnt, nt = blockIdx.x % nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nkt_total = (p.Kred + 31) / 32;
+  const int kt_begin = blockIdx.y * p.kt_per_split;
+  const int kt_end = min(nkt_total, kt_begin + p.kt_per_split);
+  if (kt_begin >= kt_end) return;
+
+  const int a_chunk = tid % ACPR, a_row = tid / ACPR;
+  const int b_chunk = tid % BCPR, b_row = tid / BCPR;
+  // this thread's patch columns: col = n0 + 8*b_chunk + e
+  const int colbase = n0 + 8 * b_chunk;
+  int b_r = 0, b_s = 0, b_c = 0;
+  if (CVEC == 8) {
+    const int rs = colbase / p.Cp;
+    b_c = colbase - rs * p.Cp;
+    b_r = rs / p.S;
+    b_s = rs - b_r * p.S;
+  }
+  const bool b_colok = colbase < p.R * p.S * p.Cp;
+  const int PQ = p.P * p.Q;
+
+  u32x4 ra[AROWS], rb[BROWS];
+  auto load_tile = [&](int kt) {
+    const int pix0 = kt * 32;
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      const int pix = pix0 + a_row + ASTEP * i;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (pix < p.Kred) v = *reinterpret_cast<const u32x4*>(p.dy + (size_t)pix * p.Mg + m0 + a_chunk * 8);
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BROWS; ++i) {
+      const int pix = pix0 + b_row + BSTEP * i;
+      const bool pok = pix < p.Kred;
+      const int pp = pok ? pix : 0;
+      const int n = pp / PQ, rem = pp - n * PQ;
+      const int oh = rem / p.Q, ow = rem - oh * p.Q;
+      const int y0 = oh * p.stride - p.pad, x0 = ow * p.stride - p.pad;
+      const bf16_t* img = p.x + (size_t)n * p.H * p.W * p.Cp;
+      if (CVEC == 8) {
+        const int y = y0 + b_r, x = x0 + b_s;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (pok && b_colok && y >= 0 && y < p.H && x >= 0 && x < p.W)
+          v = *reinterpret_cast<const u32x4*>(img + (size_t)(y * p.W + x) * p.Cp + b_c);
+        rb[i] = v;
+      } else {
+        unsigned short e[8];
+#pragma unroll
+        for (int g = 0; g < 8 / CVEC; ++g) {
+          const int pos = (colbase + g * CVEC) / CVEC;
+          const int r = pos / p.S, s = pos - r * p.S;
+          const int y = y0 + r, x = x0 + s;
+          const bool ok = pok && pos < p.R * p.S && y >= 0 && y < p.H && x >= 0 && x < p.W;
+          const bf16_t* src = img + (size_t)(y * p.W + x) * CVEC;
+          if (CVEC == 4) {
+            u32x2 v = {0u, 0u};
+            if (ok) v = *reinterpret_cast<const u32x2*>(src);
+            e[g * 4 + 0] = v.x & 0xffff;
+            e[g * 4 + 1] = v.x >> 16;
+            e[g * 4 + 2] = v.y & 0xffff;
+            e[g * 4 + 3] = v.y >> 16;
+          } else {
+            e[g] = ok ? src[0] : (unsigned short)0;
+          }
+        }
+        u32x4 v;
+        v.x = e[0] | ((unsigned)e[1] << 16);
+        v.y = e[2] | ((unsigned)e[3] << 16);
+        v.z = e[4] | ((unsigned)e[5] << 16);
+        v.w = e[6] | ((unsigned)e[7] << 16);
+        rb[i] = v;
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    bf16_t* As = smem + buf * BUF;
+    bf16_t* Bs = As + 32 * ALD;
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) *reinterpret_cast<u32x4*>(As + (a_row + ASTEP * i) * ALD + a_chunk * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BROWS; ++i) *reinterpret_cast<u32x4*>(Bs + (b_row + BSTEP * i) * BLD + b_chunk * 8) = rb[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  // tr-read lane geometry: group g = lane>>4 (16 lanes), t = lane&15 = 4q + pp
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, pq = t & 3;
+  const int tr_row = (g >> 1) * 8 + q;        // + 16*ks + 4*rr
+  const int tr_col = (g & 1) * 16 + 4 * pq;   // + tile column base
+
+  load_tile(kt_begin);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int cur = (kt - kt_begin) & 1;
+    if (kt + 1 < kt_end) load_tile(kt + 1);
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const bf16_t* As = smem + cur * BUF;
+    const bf16_t* Bs = As + 32 * ALD;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * (BM / 2) + i * 32 + tr_col;
+        const bf16_t* a0 = As + (ks * 16 + tr_row) * ALD + col;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * ALD));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, tmp);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * (BN / 2) + j * 32 + tr_col;
+        const bf16_t* b0 = Bs + (ks * 16 + tr_row) * BLD + col;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * BLD));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, tmp);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < kt_end) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: fp32 atomics into DW[k_out][(r,s,c_real)] ----
+  const int ldw = p.R * p.S * p.Creal;
+  const int frow = lane & 31, fhalf = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 32 + frow;
+    const int rs = col / p.Cp, c = col - rs * p.Cp;
+    const bool cok = rs < p.R * p.S && c < p.Creal;
+    const int dcol = rs * p.Creal + c;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        if (cok && row < p.Mg) atomicAdd(p.dw + (size_t)row * ldw + dcol, acc[i][j][v]);
+      }
+  }
+}
+
+}  // namespace avt
+
+using namespace avt;
+
+// ------------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------------
+static inline int conv_out(int in, int k, int st, int pad) { return (in + 2 * pad - k) / st + 1; }
+
+template <int MODE, int CVEC, int BM, int BN>
+static void launch_nt(const GemmNTParams& p, hipStream_t st) {
+  const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<MODE, CVEC, BM, BN>), dim3(grid), dim3(256), 0, st, p);
+}
+
+extern "C" int avt_conv2d_fwd_stat_tiles(int N, int P, int Q) { return (N * P * Q + 127) / 128; }
+
+extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, void* bn_partial, int N, int H, int W,
+                              int Cp, int K, int R, int S, int stride, int pad, int Kg, void* stream) {
+  AVT_REQUIRE(x && wpack && y, "conv2d_fwd: null pointer");
+  AVT_REQUIRE(K % 64 == 0, "conv2d_fwd: K=%d must be a multiple of 64", K);
+  AVT_REQUIRE(Kg % 32 == 0 && Kg >= R * S * Cp, "conv2d_fwd: Kg=%d must be a multiple of 32 >= R*S*C", Kg);
+  AVT_REQUIRE(Cp % 32 == 0 || Cp == 4 || Cp == 1, "conv2d_fwd: C=%d unsupported (need %%32, or stem 1/4)", Cp);
+  AVT_REQUIRE(Cp % 32 != 0 || Kg == R * S * Cp, "conv2d_fwd: Kg must equal R*S*C for C%%32==0");
+  AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_fwd: stride must be 1 or 2");
+  GemmNTParams p{};
+  p.act = (const bf16_t*)x;
+  p.wmat = (const bf16_t*)wpack;
+  p.out = (bf16_t*)y;
+  p.add = nullptr;
+  p.stats = (float2*)bn_partial;
+  p.IH = H; p.IW = W; p.IC = Cp;
+  p.OH = conv_out(H, R, stride, pad);
+  p.OW = conv_out(W, S, stride, pad);
+  p.M = N * p.OH * p.OW;
+  p.Ng = K;
+  p.Kg = Kg;
+  p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bn128 = (K % 128 == 0);
+  if (Cp == 4) {
+    launch_nt<MODE_FWD, 4, 128, 64>(p, st);
+  } else if (Cp == 1) {
+    launch_nt<MODE_FWD, 1, 128, 64>(p, st);
+  } else if (bn128) {
+    launch_nt<MODE_FWD, 8, 128, 128>(p, st);
+  } else {
+    launch_nt<MODE_FWD, 8, 128, 64>(p, st);
+  }
+  return check_launch("conv2d_fwd");
+}
+
+extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C,
+                                int K, int R, int S, int stride, int pad, void* stream) {
+  AVT_REQUIRE(dy && wt && dx, "conv2d_dgrad: null pointer");
+  AVT_REQUIRE(C % 64 == 0 && K % 32 == 0, "conv2d_dgrad: C=%d K=%d unsupported", C, K);
+  AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
+  GemmNTParams p{};
+  p.act = (const bf16_t*)dy;
+  p.wmat = (const bf16_t*)wt;
+  p.out = (bf16_t*)dx;
+  p.add = (const bf16_t*)add;
+  p.stats = nullptr;
+  p.IH = conv_out(H, R, stride, pad);
+  p.IW = conv_out(W, S, stride, pad);
+  p.IC = K;
+  p.OH = H; p.OW = W;
+  p.M = N * H * W;
+  p.Ng = C;
+  p.Kg = R * S * K;
+  p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  hipStream_t st = (hipStream_t)stream;
+  if (C % 128 == 0)
+    launch_nt<MODE_DGRAD, 8, 128, 128>(p, st);
+  else
+    launch_nt<MODE_DGRAD, 8, 128, 64>(p, st);
+  return check_launch("conv2d_dgrad");
+}
+
+template <int CVEC, int BM, int BN>
+static void launch_tn(GemmTNParams p, hipStream_t st) {
+  const int tiles = (p.Mg / BM) * (p.Ng / BN);
+  const int nkt = (p.Kred + 31) / 32;
+  int splits = (2048 + tiles - 1) / tiles;
+  int kps = (nkt + splits - 1) / splits;
+  if (kps < 4) kps = 4;
+  splits = (nkt + kps - 1) / kps;
+  p.kt_per_split = kps;
+  hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(tiles, splits), dim3(256), 0, st, p);
+}
+
+// DW must be zero-initialised (or hold a gradient to accumulate into) by the caller.
+extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
+                                int K, int R, int S, int stride, int pad, void* stream) {
+  AVT_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
+  AVT_REQUIRE(K % 64 == 0, "conv2d_wgrad: K=%d must be a multiple of 64", K);
+  AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
+  AVT_REQUIRE(Creal <= Cp, "conv2d_wgrad: Creal > Cp");
+  GemmTNParams p{};
+  p.dy = (const bf16_t*)dy;
+  p.x = (const bf16_t*)x;
+  p.dw = dw;
+  p.Mg = K;
+  p.H = H; p.W = W; p.Cp = Cp; p.Creal = Creal;
+  p.P = conv_out(H, R, stride, pad);
+  p.Q = conv_out(W, S, stride, pad);
+  p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  p.Kred = N * p.P * p.Q;
+  const int ncols = R * S * Cp;
+  hipStream_t st = (hipStream_t)stream;
+  const int BN = (ncols % 128 == 0 || ncols > 128) ? 128 : 64;
+  p.Ng = ((ncols + BN - 1) / BN) * BN;
+  const bool bm128 = (K % 128 == 0);
+  if (Cp == 4) {
+    if (bm128) launch_tn<4, 128, 128>(p, st); else launch_tn<4, 64, 128>(p, st);
+  } else if (Cp == 1) {
+    if (BN == 128) launch_tn<1, 64, 128>(p, st); else launch_tn<1, 64, 64>(p, st);
+  } else if (BN == 128) {
+    if (bm128) launch_tn<8, 128, 128>(p, st); else launch_tn<8, 64, 128>(p, st);
+  } else {
+    if (bm128) launch_tn<8, 128, 64>(p, st); else launch_tn<8, 64, 64>(p, st);
+  }
+  return check_launch("conv2d_wgrad");
+}

@@ -1,0 +1,353 @@
+// Hard-way head (fp32): per-location cosine-similarity map, sigmoid trimap, hard-negative
+// logits, cross-entropy, and their backward.  Restates model.py:114-154 (AVENet.forward after
+// the trunks) and model.py:46-60 (HardWayAttention) with the CE of train_hardway_1frame.py:130-131.
+//
+// Data: v   [B][P][C] bf16 (vision layer4, NHWC; P = h*w),  an [B][C] fp32 (unit audio vector)
+//       inv [B][P] = 1/max(||v[b,p,:]||, 1e-12),  A0 [B][P][B] fp32 (row (i,p), column j)
+// All similarity/trimap math stays fp32 (bf16 sigmoids underflow: SURVEY §0.7).
+#include "avt_common.h"
+
+namespace avt {
+
+// ---- per-(b,p) norms of the vision map: one wave per row of C channels ----
+__global__ __launch_bounds__(256) void vis_norm_kernel(const bf16_t* __restrict__ v, float* __restrict__ inv,
+                                                       float* __restrict__ vsum, int rows, int C) {
+  const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (w >= rows) return;
+  const bf16_t* src = v + (size_t)w * C;
+  float ss = 0.f, s = 0.f;
+  for (int c = lane * 8; c < C; c += 512) {
+    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
+    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = bf2f(u[e] & 0xffff), b = bf2f(u[e] >> 16);
+      ss += a * a + b * b;
+      s += a + b;
+    }
+  }
+  ss = wave_sum(ss);
+  s = wave_sum(s);
+  if (lane == 0) {
+    inv[w] = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    vsum[w] = s;
+  }
+}
+
+// ---- small fp32 GEMM with strided operands ----
+//   C[m][n] (+)= rowscale[m] * sum_k A(m,k) * kscale[k] * B(k,n)
+//   A(m,k) = a[m*sam + k*sak] (TA = bf16_t or float), B(k,n) = b[k*sbk + n*sbn] (TB)
+//   split-K over gridDim.z with fp32 atomics when gridDim.z > 1 (C pre-zeroed by caller).
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, size_t i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, size_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, size_t i) { return bf2f(p[i]); }
+
+template <typename TA, typename TB>
+__global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const TA* __restrict__ a, long long sam,
+                                                    long long sak, const TB* __restrict__ b, long long sbk,
+                                                    long long sbn, const float* __restrict__ rowscale,
+                                                    const float* __restrict__ kscale, float* __restrict__ c,
+                                                    long long ldc, int k_per_split) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int tid = threadIdx.x;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int kbeg = blockIdx.z * k_per_split, kend = min(K, kbeg + k_per_split);
+  const int tm = tid / 16, tn = tid % 16;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  const bool a_kfast = (sak == 1), b_nfast = (sbn == 1);
+  for (int k0 = kbeg; k0 < kend; k0 += 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + 256 * e;  // 1024 elements of the 64x16 A tile
+      int mm, kk;
+      if (a_kfast) {
+        mm = idx / 16;
+        kk = idx % 16;
+      } else {
+        mm = idx % 64;
+        kk = idx / 64;
+      }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float val = 0.f;
+      if (gm < M && gk < kend) {
+        val = ldf<TA>(a, (size_t)gm * sam + (size_t)gk * sak);
+        if (kscale) val *= kscale[gk];
+      }
+      As[kk][mm] = val;
+      int nn;
+      if (b_nfast) {
+        nn = idx % 64;
+        kk = idx / 64;
+      } else {
+        nn = idx / 16;
+        kk = idx % 16;
+      }
+      const int gn = n0 + nn;
+      const int gk2 = k0 + kk;
+      Bs[kk][nn] = (gn < N && gk2 < kend) ? ldf<TB>(b, (size_t)gk2 * sbk + (size_t)gn * sbn) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = As[kk][tm * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tn + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gm = m0 + tm * 4 + i;
+    if (gm >= M) continue;
+    const float rs = rowscale ? rowscale[gm] : 1.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gn = n0 + tn + 16 * j;
+      if (gn >= N) continue;
+      if (gridDim.z > 1)
+        atomicAdd(c + (size_t)gm * ldc + gn, acc[i][j] * rs);
+      else
+        c[(size_t)gm * ldc + gn] = acc[i][j] * rs;
+    }
+  }
+}
+
+__device__ __forceinline__ float sigm(float z) { return 1.f / (1.f + __expf(-z)); }
+
+// ---- logits: one block per row i ----
+// save layout (floats per row): [0..B) s_ij, [B..2B) W_ij, 2B: s1, 2B+1: W1, 2B+2: s2, 2B+3: W2
+__global__ __launch_bounds__(256) void hardway_logits_kernel(const float* __restrict__ A0, const float* __restrict__ vsum,
+                                                             const float* __restrict__ inv, int B, int P, int C,
+                                                             float eps1, float eps2, float tau, int trimap, int use_neg,
+                                                             float* __restrict__ logits, float* __restrict__ Aout,
+                                                             float* __restrict__ Pos, float* __restrict__ Neg,
+                                                             float* __restrict__ wA, float* __restrict__ save) {
+  __shared__ float red[16];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int L = B + 1 + (use_neg ? 1 : 0);
+  const float* row = A0 + (size_t)i * P * B;
+  float* sv = save + (size_t)i * (2 * B + 4);
+  const float inv_t = 1.f / tau;
+  for (int j = tid; j < B; j += blockDim.x) {
+    float sw = 0.f, swx = 0.f;
+    for (int p = 0; p < P; ++p) {
+      const float x = row[(size_t)p * B + j];
+      const float w = sigm((x - eps1) * inv_t);
+      sw += w;
+      swx += w * x;
+    }
+    const float s = swx / sw;
+    sv[j] = s;
+    sv[B + j] = sw;
+    logits[(size_t)i * L + 1 + j] = s * (j == i ? -99.f : 1.f) / 0.07f;
+  }
+  // positive / negative on A = A0[i, :, i]
+  float s1w = 0.f, s1x = 0.f, s2w = 0.f, s2x = 0.f, pp = 0.f;
+  for (int p = tid; p < P; p += blockDim.x) {
+    const float x = row[(size_t)p * B + i];
+    const float w = sigm((x - eps1) * inv_t);
+    const float wn = trimap ? sigm(-(x - eps2) * inv_t) : sigm(-(x - eps1) * inv_t);
+    s1w += w;
+    s1x += w * x;
+    s2w += wn;
+    s2x += wn * x;
+    pp += w * w;
+    Aout[(size_t)i * P + p] = x;
+    Pos[(size_t)i * P + p] = w;
+    Neg[(size_t)i * P + p] = wn;
+  }
+  s1w = block_sum(s1w, red);
+  s1x = block_sum(s1x, red);
+  s2w = block_sum(s2w, red);
+  s2x = block_sum(s2x, red);
+  pp = block_sum(pp, red);
+  const float s1 = s1x / s1w, s2 = s2x / s2w;
+  if (tid == 0) {
+    sv[2 * B] = s1;
+    sv[2 * B + 1] = s1w;
+    sv[2 * B + 2] = s2;
+    sv[2 * B + 3] = s2w;
+    logits[(size_t)i * L] = s1 / 0.07f;
+    if (use_neg) logits[(size_t)i * L + B + 1] = s2 / 0.07f;
+  }
+  // weighted_A = mean_c(vhat) * Pos / max(||Pos||, 1e-12)   (model.py:148-152)
+  const float pn = 1.f / fmaxf(sqrtf(pp), 1e-12f);
+  for (int p = tid; p < P; p += blockDim.x) {
+    const size_t r = (size_t)i * P + p;
+    wA[r] = vsum[r] * inv[r] / (float)C * Pos[r] * pn;
+  }
+}
+
+// ---- CE(target 0), mean over the B rows, times `scale`: loss and dlogits ----
+__global__ void hardway_ce_kernel(const float* __restrict__ logits, int B, int L, float scale, float* __restrict__ loss,
+                                  float* __restrict__ dlogits) {
+  __shared__ float red[16];
+  float part = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const float* r = logits + (size_t)i * L;
+    float mx = -INFINITY;
+    for (int j = 0; j < L; ++j) mx = fmaxf(mx, r[j]);
+    float se = 0.f;
+    for (int j = 0; j < L; ++j) se += __expf(r[j] - mx);
+    const float lse = mx + __logf(se);
+    part += lse - r[0];
+    if (dlogits) {
+      for (int j = 0; j < L; ++j) {
+        const float sm = __expf(r[j] - lse);
+        dlogits[(size_t)i * L + j] = (sm - (j == 0 ? 1.f : 0.f)) * scale / (float)B;
+      }
+    }
+  }
+  const float tot = block_sum(part, red);
+  if (threadIdx.x == 0 && loss) *loss = tot / (float)B;
+}
+
+// ---- backward of the logits w.r.t. A0: one block per row i; dA0 [B][P][B] ----
+__global__ __launch_bounds__(256) void hardway_logits_bwd_kernel(const float* __restrict__ A0,
+                                                                 const float* __restrict__ save,
+                                                                 const float* __restrict__ dlogits, int B, int P,
+                                                                 float eps1, float eps2, float tau, int trimap,
+                                                                 int use_neg, float* __restrict__ dA0) {
+  const int i = blockIdx.x;
+  const int L = B + 1 + (use_neg ? 1 : 0);
+  const float* row = A0 + (size_t)i * P * B;
+  float* drow = dA0 + (size_t)i * P * B;
+  const float* sv = save + (size_t)i * (2 * B + 4);
+  const float inv_t = 1.f / tau;
+  const float* dl = dlogits + (size_t)i * L;
+  const float s1 = sv[2 * B], W1 = sv[2 * B + 1], s2 = sv[2 * B + 2], W2 = sv[2 * B + 3];
+  const float ds1 = dl[0] / 0.07f;
+  const float ds2 = use_neg ? dl[B + 1] / 0.07f : 0.f;
+  const size_t n = (size_t)P * B;
+  for (size_t t = threadIdx.x; t < n; t += blockDim.x) {
+    const int j = (int)(t % B);
+    const float x = row[t];
+    const float w = sigm((x - eps1) * inv_t);
+    const float wd = w * (1.f - w) * inv_t;
+    const float dsim = dl[1 + j] * (j == i ? -99.f : 1.f) / 0.07f;
+    float g = dsim * (w + wd * (x - sv[j])) / sv[B + j];
+    if (j == i) {
+      g += ds1 * (w + wd * (x - s1)) / W1;
+      if (use_neg) {
+        const float wn = trimap ? sigm(-(x - eps2) * inv_t) : sigm(-(x - eps1) * inv_t);
+        const float wnd = -wn * (1.f - wn) * inv_t;
+        g += ds2 * (wn + wnd * (x - s2)) / W2;
+      }
+    }
+    drow[t] = g;
+  }
+}
+
+// ---- normalize backward for the vision map: gv = inv*(dvh - vh*<vh,dvh>), vh = v*inv ----
+__global__ __launch_bounds__(256) void vis_norm_bwd_kernel(const bf16_t* __restrict__ v, const float* __restrict__ inv,
+                                                           const float* __restrict__ dvh, bf16_t* __restrict__ gv,
+                                                           int rows, int C) {
+  const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (w >= rows) return;
+  const bf16_t* src = v + (size_t)w * C;
+  const float* d = dvh + (size_t)w * C;
+  const float iv = inv[w];
+  float dot = 0.f;
+  for (int c = lane * 8; c < C; c += 512) {
+    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
+    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += bf2f(u[e] & 0xffff) * d[c + 2 * e] + bf2f(u[e] >> 16) * d[c + 2 * e + 1];
+  }
+  dot = wave_sum(dot) * iv;  // <vh, dvh>
+  for (int c = lane * 8; c < C; c += 512) {
+    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
+    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
+    u32x4 o;
+    unsigned* ou = reinterpret_cast<unsigned*>(&o);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = iv * (d[c + 2 * e] - bf2f(u[e] & 0xffff) * iv * dot);
+      const float b = iv * (d[c + 2 * e + 1] - bf2f(u[e] >> 16) * iv * dot);
+      ou[e] = pack2(a, b);
+    }
+    *reinterpret_cast<u32x4*>(gv + (size_t)w * C + c) = o;
+  }
+}
+
+template <typename TA, typename TB>
+static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak, const TB* b, long long sbk,
+                  long long sbn, const float* rowscale, const float* kscale, float* c, long long ldc, int splits,
+                  hipStream_t st) {
+  int kps = (K + splits - 1) / splits;
+  kps = ((kps + 15) / 16) * 16;
+  splits = (K + kps - 1) / kps;
+  dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
+  hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
+                     kscale, c, ldc, kps);
+}
+
+}  // namespace avt
+
+using namespace avt;
+
+extern "C" size_t avt_hardway_save_floats(int B) { return (size_t)B * (2 * B + 4); }
+
+// Forward of the hard-way head from the trunk outputs.
+//   v [B][P][C] bf16, an [B][C] fp32 (unit audio vectors)
+//   outputs: logits [B][B+2|B+1], A/Pos/Neg/wA [B][P]
+//   saved for backward: inv [B][P], vsum [B][P], A0 [B][P][B], save [B][2B+4]
+extern "C" int avt_hardway_fwd(const void* v, const float* an, int B, int P, int C, float eps1, float eps2, float tau,
+                               int trimap, int use_neg, float* inv, float* vsum, float* A0, float* save, float* logits,
+                               float* Aout, float* Pos, float* Neg, float* wA, void* stream) {
+  AVT_REQUIRE(v && an && inv && vsum && A0 && save && logits && Aout && Pos && Neg && wA, "hardway_fwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && B >= 1 && P >= 1, "hardway_fwd: bad shape B=%d P=%d C=%d", B, P, C);
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = B * P;
+  hipLaunchKernelGGL(vis_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, vsum, rows, C);
+  // A0[(i,p)][j] = inv[(i,p)] * sum_c v[(i,p)][c] * an[j][c]
+  sgemm<bf16_t, float>(rows, B, C, (const bf16_t*)v, C, 1, an, 1, C, inv, nullptr, A0, B, 1, st);
+  hipLaunchKernelGGL(hardway_logits_kernel, dim3(B), dim3(256), 0, st, A0, vsum, inv, B, P, C, eps1, eps2, tau, trimap,
+                     use_neg, logits, Aout, Pos, Neg, wA, save);
+  return check_launch("hardway_fwd");
+}
+
+extern "C" int avt_hardway_ce(const float* logits, int B, int L, float scale, float* loss, float* dlogits,
+                              void* stream) {
+  AVT_REQUIRE(logits, "hardway_ce: null pointer");
+  hipLaunchKernelGGL(hardway_ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, B, L, scale, loss, dlogits);
+  return check_launch("hardway_ce");
+}
+
+// Backward from dlogits to the trunk outputs.
+//   workspace: dA0 [B][P][B] fp32 + dvh [B][P][C] fp32
+//   outputs: gv [B][P][C] bf16 (grad of the vision layer4 map), gan [B][C] fp32 (grad of the unit audio vectors)
+extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
+                               const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
+                               int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream) {
+  AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && dvh && gv && gan, "hardway_bwd: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = B * P;
+  hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2, tau,
+                     trimap, use_neg, dA0);
+  // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]
+  sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
+  // gan[j][c] = sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
+  (void)hipMemsetAsync(gan, 0, (size_t)B * C * sizeof(float), st);
+  int splits = rows / 256;
+  if (splits < 1) splits = 1;
+  if (splits > 64) splits = 64;
+  sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st);
+  hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
+                     (bf16_t*)gv, rows, C);
+  return check_launch("hardway_bwd");
+}

@@ -1,0 +1,171 @@
+// Optimizer, weight packing, input layout and error plumbing for libavt.
+//  * Adam with coupled L2 weight decay over one flat fp32 buffer (torch.optim.Adam semantics as
+//    constructed at train_hardway_1frame.py:116 and stepped at :134).
+//  * Weight packing: fp32 master weights (OHWI memory order, i.e. channels_last OIHW params) ->
+//    bf16 fwd operand [K][Kg] (stem channels padded) and bf16 dgrad operand [C][R*S*K].
+//  * Input layout: fp32 NCHW (the reference's frames.float()/spec.float(), train_hardway_1frame.py:129)
+//    -> bf16 NHWC with channels padded to Cp.
+#include "avt_common.h"
+#include <stdarg.h>
+
+namespace avt {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return AVT_EHIP;
+  }
+  return AVT_OK;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long long n,
+                                                   float gscale, float b1, float b2, float eps, float wd,
+                                                   float step_size, float bc2_sqrt) {
+  const long long nv = n / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gg = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gr = gg[e] * gscale + wd * pp[e];
+      mm[e] = b1 * mm[e] + (1.f - b1) * gr;
+      vv[e] = b2 * vv[e] + (1.f - b2) * gr * gr;
+      const float denom = sqrtf(vv[e]) / bc2_sqrt + eps;
+      pp[e] = pp[e] - step_size * mm[e] / denom;
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pp;
+    reinterpret_cast<f32x4*>(m)[i] = mm;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  // tail
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = nv * 4 + threadIdx.x;
+    const float gr = g[i] * gscale + wd * p[i];
+    m[i] = b1 * m[i] + (1.f - b1) * gr;
+    v[i] = b2 * v[i] + (1.f - b2) * gr * gr;
+    p[i] = p[i] - step_size * m[i] / (sqrtf(v[i]) / bc2_sqrt + eps);
+  }
+}
+
+// w: [K][R][S][C] fp32 -> fwd [K][Kg] bf16 with (r,s,c<Cp) packing, zero for c>=C and k>=R*S*Cp
+__global__ void pack_fwd_kernel(const float* __restrict__ w, bf16_t* __restrict__ out, int K, int RS, int C, int Cp,
+                                int Kg) {
+  const long long total = (long long)K * Kg;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t / Kg), col = (int)(t % Kg);
+    const int rs = col / Cp, c = col % Cp;
+    float val = 0.f;
+    if (rs < RS && c < C) val = w[((size_t)k * RS + rs) * C + c];
+    out[t] = f2bf(val);
+  }
+}
+
+// w: [K][R][S][C] fp32 -> dgrad [C][R][S][K] bf16
+__global__ void pack_dgrad_kernel(const float* __restrict__ w, bf16_t* __restrict__ out, int K, int RS, int C) {
+  const long long total = (long long)K * RS * C;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % K);
+    const long long r2 = t / K;
+    const int rs = (int)(r2 % RS), c = (int)(r2 / RS);
+    out[t] = f2bf(w[((size_t)k * RS + rs) * C + c]);
+  }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W,
+                                    int Cp) {
+  const long long total = (long long)N * H * W;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(t / ((long long)H * W));
+    const long long hw = t % ((long long)H * W);
+    for (int c = 0; c < Cp; ++c) {
+      const float v = c < C ? x[((size_t)n * C + c) * H * W + hw] : 0.f;
+      y[t * Cp + c] = f2bf(v);
+    }
+  }
+}
+
+// NHWC bf16 -> NCHW fp32 (hooks / returning trunk maps in the reference layout)
+__global__ void nhwc_to_nchw_kernel(const bf16_t* __restrict__ x, float* __restrict__ y, int N, int C, int HW) {
+  const long long total = (long long)N * C * HW;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const int hw = (int)(t % HW);
+    const long long r = t / HW;
+    const int c = (int)(r % C), n = (int)(r / C);
+    y[t] = bf2f(x[((size_t)n * HW + hw) * C + c]);
+  }
+}
+
+static int grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace avt
+
+using namespace avt;
+
+extern "C" const char* avt_last_error(void) { return g_err; }
+
+extern "C" int avt_abi_version(void) { return 1; }
+
+// torch.optim.Adam (amsgrad=False, maximize=False) with coupled L2 weight decay on one flat segment;
+// grad is multiplied by grad_scale first (1/world for a summed all-reduce).
+extern "C" int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                             float grad_scale, float lr, float beta1, float beta2, float eps, float weight_decay,
+                             int step, void* stream) {
+  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq, "adam_step: null pointer");
+  AVT_REQUIRE(step >= 1, "adam_step: step must be >= 1");
+  AVT_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+              "adam_step: buffers must be 16-byte aligned");
+  if (n == 0) return AVT_OK;
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, n, grad_scale, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
+  return check_launch("adam_step");
+}
+
+extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd,
+                                    void* out_dgrad, void* stream) {
+  AVT_REQUIRE(w, "pack_conv_weight: null pointer");
+  AVT_REQUIRE(Cp >= C && Kg >= R * S * Cp, "pack_conv_weight: bad padding");
+  hipStream_t st = (hipStream_t)stream;
+  if (out_fwd)
+    hipLaunchKernelGGL(pack_fwd_kernel, dim3(grid_for((long long)K * Kg)), dim3(256), 0, st, w, (bf16_t*)out_fwd, K,
+                       R * S, C, Cp, Kg);
+  if (out_dgrad)
+    hipLaunchKernelGGL(pack_dgrad_kernel, dim3(grid_for((long long)K * R * S * C)), dim3(256), 0, st, w,
+                       (bf16_t*)out_dgrad, K, R * S, C);
+  return check_launch("pack_conv_weight");
+}
+
+extern "C" int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream) {
+  AVT_REQUIRE(x && y && Cp >= C, "nchw_to_nhwc_bf16: bad arguments");
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)N * H * W)), dim3(256), 0, (hipStream_t)stream, x,
+                     (bf16_t*)y, N, C, H, W, Cp);
+  return check_launch("nchw_to_nhwc_bf16");
+}
+
+extern "C" int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream) {
+  AVT_REQUIRE(x && y, "nhwc_bf16_to_nchw: null pointer");
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for((long long)N * C * HW)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, y, N, C, HW);
+  return check_launch("nhwc_bf16_to_nchw");
+}

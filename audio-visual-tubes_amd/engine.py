@@ -1,0 +1,272 @@
+"""AVENet train/eval step on libavt: flat parameter storage, forward with a tape, backward into a
+flat fp32 gradient buffer.
+
+Data flow of one 1-frame step (model.py:112-154, train_hardway_1frame.py:129-134):
+  image [B,3,H,W] fp32 NCHW --avt_nchw_to_nhwc_bf16--> [B,H,W,4] bf16 --Trunk(vision)--> v [B,h,w,512]
+  audio [B,1,F,T] fp32       --avt_nchw_to_nhwc_bf16--> [B,F,T,1] bf16 --Trunk(audio)--> a [B,h',w',512]
+  a --avt_audio_pool_norm_fwd--> an [B,512];  (v, an) --avt_hardway_fwd--> A, logits, weighted_A, Pos, Neg
+  CE (avt_hardway_ce) -> dlogits --avt_hardway_bwd--> gv, g_an --> trunk backward --> flat grads --> Adam.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ._lib import call, query
+from .trunk import P, Store, Trunk, stream_ptr
+
+# ---------------------------------------------------------------------------------------------
+# parameter inventory (state_dict of the reference AVENet, model.py:89-110 + base_models.py:113-169)
+# ---------------------------------------------------------------------------------------------
+
+
+def trainable(name: str) -> bool:
+    """Parameters that receive gradients on the 1-frame step: everything except both fc layers,
+    both conv1_flow stems and the other modality's stem (SURVEY §7 'Unused parameters')."""
+    if ".fc." in name or name.endswith("conv1_flow.weight"):
+        return False
+    if name.startswith("imgnet.") and name.endswith("conv1_a.weight"):
+        return False
+    if name.startswith("audnet.conv1.weight"):
+        return False
+    return True
+
+
+class FlatStore:
+    """All parameters of a module in one flat fp32 buffer (trainable ones first), all float
+    buffers in a second one, num_batches_tracked counters in a third.  Conv weights are kept in
+    OHWI memory order, exposed as channels_last OIHW ``nn.Parameter`` views, so the kernels read
+    them directly and ``state_dict``/``load_state_dict`` keep the reference's key names and shapes."""
+
+    def __init__(self, module: torch.nn.Module):
+        self.module = module
+        params = [(n, p) for n, p in module.named_parameters()]
+        order = [x for x in params if trainable(x[0])] + [x for x in params if not trainable(x[0])]
+        self.pnames = [n for n, _ in order]
+        self.n_train = 0
+        self.poff: Dict[str, Tuple[int, tuple]] = OrderedDict()
+        off = 0
+        for n, p in order:
+            if trainable(n):
+                self.n_train = off + p.numel()
+            self.poff[n] = (off, tuple(p.shape))
+            off += (p.numel() + 3) // 4 * 4  # 16-byte aligned segments
+        self.n_train = (self.n_train + 3) // 4 * 4
+        device = params[0][1].device
+        self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        self.boff: Dict[str, Tuple[int, tuple]] = OrderedDict()
+        self.nbt_names: List[str] = []
+        boff = 0
+        for n, b in module.named_buffers():
+            if n.endswith("num_batches_tracked"):
+                self.nbt_names.append(n)
+                continue
+            self.boff[n] = (boff, tuple(b.shape))
+            boff += b.numel()
+        self.bflat = torch.zeros(max(boff, 1), dtype=torch.float32, device=device)
+        self.nbt = torch.zeros(len(self.nbt_names), dtype=torch.long, device=device)
+        with torch.no_grad():
+            for n, p in params:
+                src = p.detach().float()
+                self.raw(n).copy_(src.permute(0, 2, 3, 1) if src.dim() == 4 else src)
+            for n, b in module.named_buffers():
+                if n in self.boff:
+                    self.rawbuf(n).copy_(b.detach().float().reshape(-1))
+                elif n in self.nbt_names:
+                    self.nbt[self.nbt_names.index(n)] = b.detach().long()
+        self.rebind()
+
+    def raw(self, name: str) -> torch.Tensor:
+        """fp32 storage of a parameter: conv weights as [K][R][S][C] (OHWI), others as-is."""
+        off, shape = self.poff[name]
+        n = 1
+        for s in shape:
+            n *= s
+        t = self.flat[off:off + n]
+        if len(shape) == 4:
+            k, c, r, s = shape
+            return t.view(k, r, s, c)
+        return t.view(shape)
+
+    def rawbuf(self, name: str) -> torch.Tensor:
+        off, shape = self.boff[name]
+        n = 1
+        for s in shape:
+            n *= s
+        return self.bflat[off:off + n].view(shape)
+
+    def _pview(self, name: str) -> torch.Tensor:
+        r = self.raw(name)
+        return r.permute(0, 3, 1, 2) if r.dim() == 4 else r
+
+    def rebind(self):
+        """(Re)point every registered Parameter/buffer of the module at the flat storage."""
+        mods = dict(self.module.named_modules())
+        for n in self.pnames:
+            mname, _, pname = n.rpartition(".")
+            m = mods[mname]
+            old = m._parameters[pname]
+            m._parameters[pname] = torch.nn.Parameter(self._pview(n), requires_grad=old.requires_grad)
+        for n in self.boff:
+            mname, _, bname = n.rpartition(".")
+            mods[mname]._buffers[bname] = self.rawbuf(n)
+        for i, n in enumerate(self.nbt_names):
+            mname, _, bname = n.rpartition(".")
+            mods[mname]._buffers[bname] = self.nbt[i]
+
+    def apply(self, fn):
+        self.flat = fn(self.flat)
+        self.bflat = fn(self.bflat)
+        self.nbt = fn(self.nbt)
+        if self.flat.dtype != torch.float32 or self.bflat.dtype != torch.float32:
+            raise TypeError("avt AVENet keeps fp32 master weights; dtype casts are not supported "
+                            "(the trunks compute in bf16 with fp32 statistics)")
+        self.rebind()
+
+    def grad_views(self, gflat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        out = {}
+        for n in self.pnames:
+            if not trainable(n):
+                continue
+            off, shape = self.poff[n]
+            k = 1
+            for s in shape:
+                k *= s
+            t = gflat[off:off + k]
+            out[n] = t.view(shape[0], shape[2], shape[3], shape[1]) if len(shape) == 4 else t.view(shape)
+        return out
+
+    def param_grad_views(self, gflat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """gradient views shaped/strided like the Parameters (channels_last OIHW)."""
+        return {n: (g.permute(0, 3, 1, 2) if g.dim() == 4 else g) for n, g in self.grad_views(gflat).items()}
+
+
+class _EngineStore(Store):
+    def __init__(self, engine: "AVEngine"):
+        self.e = engine
+        self.grads: Optional[Dict[str, torch.Tensor]] = None
+
+    def param(self, name):
+        return self.e.flat.raw(name)
+
+    def buffer(self, name):
+        return self.e.flat.rawbuf(name)
+
+    def grad(self, name):
+        return self.grads[name]
+
+    def packed(self, spec):
+        return self.e.packs[spec.name]
+
+
+class AVEngine:
+    """Two trunks + the hard-way head on one device."""
+
+    def __init__(self, flat: FlatStore, epsilon=0.65, epsilon2=0.4, tau=0.03, tri_map=True, neg=True):
+        self.flat = flat
+        self.img = Trunk("imgnet.", "vision")
+        self.aud = Trunk("audnet.", "audio")
+        self.epsilon, self.epsilon2, self.tau, self.tri_map, self.neg = epsilon, epsilon2, tau, tri_map, neg
+        self.store = _EngineStore(self)
+        self.packs: Dict[str, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
+
+    # ----------------------------------------------------------------------------- weights
+    def pack_weights(self):
+        dev = self.flat.flat.device
+        for tr in (self.img, self.aud):
+            for spec in tr.convs():
+                w = self.flat.raw(spec.name)
+                if spec.name not in self.packs or self.packs[spec.name][0].device != dev:
+                    wf = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+                    wt = None if spec.is_stem else torch.empty(spec.cin, spec.k * spec.k * spec.cout, device=dev,
+                                                               dtype=torch.bfloat16)
+                    self.packs[spec.name] = (wf, wt)
+                wf, wt = self.packs[spec.name]
+                call("avt_pack_conv_weight", P(w), spec.cout, spec.k, spec.k, spec.cin, spec.cp, spec.kg, P(wf), P(wt),
+                     stream_ptr())
+
+    # ----------------------------------------------------------------------------- forward
+    @staticmethod
+    def _to_nhwc(x: torch.Tensor, cp: int) -> torch.Tensor:
+        x = x.contiguous().float()
+        N, C, H, W = x.shape
+        y = torch.empty(N, H, W, cp, device=x.device, dtype=torch.bfloat16)
+        call("avt_nchw_to_nhwc_bf16", P(x), P(y), N, C, H, W, cp, stream_ptr())
+        return y
+
+    def forward(self, image: torch.Tensor, audio: torch.Tensor, training: bool, with_ce: bool = False,
+                ce_scale: float = 1.0):
+        if not image.is_cuda or not audio.is_cuda:
+            raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
+        if image.shape[1] != 3 or audio.shape[1] != 1:
+            raise ValueError(f"avt: expected image [B,3,H,W] and audio [B,1,F,T], got {tuple(image.shape)} "
+                             f"and {tuple(audio.shape)}")
+        B = image.shape[0]
+        if audio.shape[0] != B:
+            raise ValueError("avt: image and audio batch sizes differ")
+        self.pack_weights()
+        if training:
+            self.flat.nbt.add_(1)
+        xi = self._to_nhwc(image, 4)
+        xa = self._to_nhwc(audio, 1)
+        v, tape_i = self.img.forward(xi, self.store, training)
+        a, tape_a = self.aud.forward(xa, self.store, training)
+        dev = image.device
+        _, h, w, C = v.shape
+        Pn = h * w
+        an = torch.empty(B, C, device=dev, dtype=torch.float32)
+        amax = torch.empty(B, C, device=dev, dtype=torch.int32)
+        anorm = torch.empty(B, device=dev, dtype=torch.float32)
+        call("avt_audio_pool_norm_fwd", P(a), P(an), P(amax), P(anorm), B, a.shape[1] * a.shape[2], C, stream_ptr())
+        L = B + (2 if self.neg else 1)
+        f32 = dict(device=dev, dtype=torch.float32)
+        inv = torch.empty(B, Pn, **f32)
+        vsum = torch.empty(B, Pn, **f32)
+        A0 = torch.empty(B, Pn, B, **f32)
+        save = torch.empty(int(query("avt_hardway_save_floats", B)), **f32)
+        logits = torch.empty(B, L, **f32)
+        A = torch.empty(B, 1, h, w, **f32)
+        Pos = torch.empty(B, 1, h, w, **f32)
+        Neg = torch.empty(B, 1, h, w, **f32)
+        wA = torch.empty(B, h, w, **f32)
+        call("avt_hardway_fwd", P(v), P(an), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map),
+             int(self.neg), P(inv), P(vsum), P(A0), P(save), P(logits), P(A), P(Pos), P(Neg), P(wA), stream_ptr())
+        out = {"A": A, "logits": logits, "weighted_A": wA, "Pos": Pos, "Neg": Neg, "v": v}
+        tape = None
+        if training:
+            tape = {"img": tape_i, "aud": tape_a, "v": v, "a": a, "an": an, "amax": amax, "anorm": anorm,
+                    "inv": inv, "A0": A0, "save": save, "B": B, "P": Pn, "C": C}
+        if with_ce:
+            loss = torch.empty((), **f32)
+            dlogits = torch.empty(B, L, **f32) if training else None
+            call("avt_hardway_ce", P(logits), B, L, ce_scale, P(loss), P(dlogits), stream_ptr())
+            out["loss"] = loss
+            out["dlogits"] = dlogits
+        return out, tape
+
+    # ----------------------------------------------------------------------------- backward
+    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor):
+        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it)."""
+        B, Pn, C = tape["B"], tape["P"], tape["C"]
+        dev = dlogits.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        dA0 = torch.empty(B, Pn, B, **f32)
+        dvh = torch.empty(B, Pn, C, **f32)
+        gv = torch.empty_like(tape["v"])
+        gan = torch.empty(B, C, **f32)
+        dlogits = dlogits.contiguous().float()
+        call("avt_hardway_bwd", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
+             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map), int(self.neg), P(dA0),
+             P(dvh), P(gv), P(gan), stream_ptr())
+        a = tape["a"]
+        ga = torch.empty_like(a)
+        call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
+             a.shape[1] * a.shape[2], C, stream_ptr())
+        self.store.grads = self.flat.grad_views(gflat)
+        try:
+            self.img.backward(tape["img"], gv, self.store)
+            self.aud.backward(tape["aud"], ga, self.store)
+        finally:
+            self.store.grads = None

@@ -1,0 +1,48 @@
+"""Fused hard-way train step: forward + CE + backward + (RCCL all-reduce) + Adam, no autograd.
+
+Equivalent to one iteration of train_hardway_1frame.py:121-135 with the model wrapped for data
+parallelism.  The reference uses ``nn.DataParallel`` (train_hardway_1frame.py:93): each replica
+contrasts only its own B/G samples (model.py:114-115) and gradients are reduced to GPU 0.  Here
+each process owns one GPU and its local batch (same local-negative semantics), gradients are
+averaged with ONE all-reduce of the flat fp32 gradient buffer over RCCL (backend "nccl"), and BN
+running statistics follow rank 0 (DDP ``broadcast_buffers``, matching DP's replica-0 buffers).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .engine import AVEngine
+from .optim import FlatAdam
+
+
+class HardWayTrainStep:
+    def __init__(self, model, lr: float = 1e-6, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 process_group: Optional[dist.ProcessGroup] = None):
+        self.model = model
+        self.engine: AVEngine = model.engine()
+        self.flat = model._flat
+        self.opt = FlatAdam(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        self.grad = torch.zeros(self.flat.n_train, device=self.flat.flat.device, dtype=torch.float32)
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        if self.world > 1:
+            # start from identical weights everywhere (DDP constructor semantics)
+            dist.broadcast(self.flat.flat, 0, group=self.pg)
+            dist.broadcast(self.flat.bflat, 0, group=self.pg)
+
+    def step(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
+        """Returns the local mean CE loss (device scalar, no host sync)."""
+        if self.world > 1:
+            dist.broadcast(self.flat.bflat, 0, group=self.pg)  # BN running stats follow rank 0
+        out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
+        self.grad.zero_()
+        self.engine.backward(tape, out["dlogits"], self.grad)
+        scale = 1.0
+        if self.world > 1:
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            scale = 1.0 / self.world
+        self.opt.step(self.grad, grad_scale=scale)
+        return out["loss"]

@@ -1,0 +1,281 @@
+"""ResNet-18 trunk (one modality) as a sequence of libavt launches: forward with a saved tape,
+backward into flat fp32 gradients.
+
+Restates models/base_models.py: ResNet._forward_impl (195-210) with the modal-selected stem
+(conv1 3->64 for vision, conv1_a 1->64 for audio, 7x7/s2/p3), bn1, ReLU, MaxPool(3,2,1),
+layer1..4 of BasicBlocks (53-69) with layer4 stride 1 (149).  Activations are NHWC bf16 held in
+torch.bfloat16 tensors (raw bits shared with the kernels); BN statistics fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from ._lib import call, query
+
+STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
+
+
+def P(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def conv_out(n: int, k: int, s: int, p: int) -> int:
+    return (n + 2 * p - k) // s + 1
+
+
+class ConvProfiler:
+    """Optional HIP-event bracketing of every conv launch (bench.py's live roofline).
+    Records (kind, algorithmic FLOPs, start, end) on the launching stream."""
+
+    active: Optional["ConvProfiler"] = None
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        ConvProfiler.active = self
+        return self
+
+    def __exit__(self, *exc):
+        ConvProfiler.active = None
+
+    @staticmethod
+    def begin():
+        p = ConvProfiler.active
+        if p is None:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    @staticmethod
+    def end(ev, kind: str, flops: float):
+        p = ConvProfiler.active
+        if p is None or ev is None:
+            return
+        e2 = torch.cuda.Event(enable_timing=True)
+        e2.record()
+        p.records.append((kind, flops, ev, e2))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, fl, a, b in self.records:
+            ms = a.elapsed_time(b)
+            k = out.setdefault(kind, [0, 0.0, 0.0])
+            k[0] += 1
+            k[1] += fl
+            k[2] += ms
+        return out
+
+
+@dataclass
+class ConvSpec:
+    name: str      # parameter name (state_dict key of the weight)
+    cin: int       # real input channels
+    cout: int
+    k: int
+    stride: int
+    pad: int
+    cp: int        # padded input channels in the activation layout (stems: 4 / 1)
+
+    @property
+    def kg(self) -> int:
+        kg = self.k * self.k * self.cp
+        return (kg + 31) // 32 * 32
+
+    @property
+    def is_stem(self) -> bool:
+        return self.cp < 32
+
+
+@dataclass
+class BNSpec:
+    prefix: str
+    c: int
+
+
+class Store:
+    """Where a trunk finds its tensors: fp32 params (conv weights OHWI-contiguous), BN buffers,
+    packed bf16 weights, and (during backward) fp32 gradient views."""
+
+    def param(self, name: str) -> torch.Tensor: ...
+    def buffer(self, name: str) -> torch.Tensor: ...
+    def grad(self, name: str) -> Optional[torch.Tensor]: ...
+    def packed(self, spec: ConvSpec): ...
+
+
+def _bn_finalize(c_out, partial, tiles, rows, bn: BNSpec, store: Store, training: bool, momentum=0.1, eps=1e-5):
+    C = bn.c
+    stats = torch.empty(4, C, device=c_out.device, dtype=torch.float32)  # scale, shift, mean, invstd
+    gamma = store.param(bn.prefix + ".weight")
+    beta = store.param(bn.prefix + ".bias")
+    if training:
+        call("avt_bn_finalize", P(partial), tiles, rows, 128, C, P(gamma), P(beta),
+             P(store.buffer(bn.prefix + ".running_mean")), P(store.buffer(bn.prefix + ".running_var")),
+             ctypes.c_float(momentum), ctypes.c_float(eps), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]),
+             stream_ptr())
+    else:
+        rm = store.buffer(bn.prefix + ".running_mean")
+        rv = store.buffer(bn.prefix + ".running_var")
+        inv = torch.rsqrt(rv + eps)
+        stats[0] = gamma * inv
+        stats[1] = beta - rm * stats[0]
+        stats[2] = rm
+        stats[3] = inv
+    return stats
+
+
+class Trunk:
+    """One ResNet-18 (base_models.resnet18(modal=...)) on libavt."""
+
+    def __init__(self, prefix: str, modal: str):
+        self.prefix, self.modal = prefix, modal
+        if modal == "audio":
+            self.stem = ConvSpec(prefix + "conv1_a.weight", 1, 64, 7, 2, 3, 1)
+        else:
+            self.stem = ConvSpec(prefix + "conv1.weight", 3, 64, 7, 2, 3, 4)
+        self.bn1 = BNSpec(prefix + "bn1", 64)
+        self.blocks = []
+        inplanes = 64
+        for li, (planes, stride) in enumerate(STAGES, start=1):
+            for bi in range(2):
+                s = stride if bi == 0 else 1
+                p = f"{prefix}layer{li}.{bi}."
+                cin = inplanes if bi == 0 else planes
+                blk = {
+                    "conv1": ConvSpec(p + "conv1.weight", cin, planes, 3, s, 1, cin),
+                    "bn1": BNSpec(p + "bn1", planes),
+                    "conv2": ConvSpec(p + "conv2.weight", planes, planes, 3, 1, 1, planes),
+                    "bn2": BNSpec(p + "bn2", planes),
+                    "down": None,
+                    "bnd": None,
+                }
+                if bi == 0 and (s != 1 or inplanes != planes):
+                    blk["down"] = ConvSpec(p + "downsample.0.weight", inplanes, planes, 1, s, 0, inplanes)
+                    blk["bnd"] = BNSpec(p + "downsample.1", planes)
+                self.blocks.append(blk)
+            inplanes = planes
+
+    def convs(self) -> List[ConvSpec]:
+        out = [self.stem]
+        for b in self.blocks:
+            out += [b["conv1"], b["conv2"]] + ([b["down"]] if b["down"] is not None else [])
+        return out
+
+    def bns(self) -> List[BNSpec]:
+        out = [self.bn1]
+        for b in self.blocks:
+            out += [b["bn1"], b["bn2"]] + ([b["bnd"]] if b["bnd"] is not None else [])
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool):
+        Pq, Qq = conv_out(H, spec.k, spec.stride, spec.pad), conv_out(W, spec.k, spec.stride, spec.pad)
+        y = torch.empty(N, Pq, Qq, spec.cout, device=x.device, dtype=torch.bfloat16)
+        tiles = query("avt_conv2d_fwd_stat_tiles", N, Pq, Qq)
+        partial = torch.empty(tiles, spec.cout, 2, device=x.device, dtype=torch.float32) if training else None
+        wf, _ = store.packed(spec)
+        ev = ConvProfiler.begin()
+        call("avt_conv2d_fwd", P(x), P(wf), P(y), P(partial), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
+             spec.stride, spec.pad, spec.kg, stream_ptr())
+        ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin)
+        stats = _bn_finalize(y, partial, tiles, N * Pq * Qq, bn, store, training)
+        return y, stats, Pq, Qq
+
+    def forward(self, x: torch.Tensor, store: Store, training: bool):
+        """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape)."""
+        N, H, W, _ = x.shape
+        tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
+        c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
+        h0 = torch.empty_like(c0)
+        call("avt_bn_apply", P(c0), P(st0[0]), P(st0[1]), None, None, None, P(h0), N * H1 * W1, 64, 1, stream_ptr())
+        H2, W2 = conv_out(H1, 3, 2, 1), conv_out(W1, 3, 2, 1)
+        p0 = torch.empty(N, H2, W2, 64, device=x.device, dtype=torch.bfloat16)
+        idx = torch.empty(N, H2, W2, 64, device=x.device, dtype=torch.uint8)
+        call("avt_maxpool3s2_fwd", P(h0), P(p0), P(idx), N, H1, W1, 64, stream_ptr())
+        tape.update(c0=c0, st0=st0, h0=h0, idx=idx, H1=H1, W1=W1)
+        cur, Hc, Wc = p0, H2, W2
+        for blk in self.blocks:
+            t = {"x": cur, "H": Hc, "W": Wc}
+            c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
+            h1 = torch.empty_like(c1)
+            call("avt_bn_apply", P(c1), P(s1[0]), P(s1[1]), None, None, None, P(h1), N * Ho * Wo, c1.shape[-1], 1,
+                 stream_ptr())
+            c2, s2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training)
+            out = torch.empty_like(c2)
+            if blk["down"] is not None:
+                cd, sd, _, _ = self._conv_bn(cur, N, Hc, Wc, blk["down"], blk["bnd"], store, training)
+                call("avt_bn_apply", P(c2), P(s2[0]), P(s2[1]), P(cd), P(sd[0]), P(sd[1]), P(out), N * Ho * Wo,
+                     c2.shape[-1], 1, stream_ptr())
+                t.update(cd=cd, sd=sd)
+            else:
+                call("avt_bn_apply", P(c2), P(s2[0]), P(s2[1]), P(cur), None, None, P(out), N * Ho * Wo, c2.shape[-1],
+                     1, stream_ptr())
+            t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, Ho=Ho, Wo=Wo)
+            tape["blocks"].append(t)
+            cur, Hc, Wc = out, Ho, Wo
+        if not training:
+            tape = None
+        return cur, tape
+
+    # ------------------------------------------------------------------ backward
+    def _bn_bwd(self, g, y, xc, stats, bn: BNSpec, store: Store, gmask_out=None):
+        rows = xc.numel() // bn.c
+        gc = torch.empty_like(xc)
+        ws = torch.empty(int(query("avt_bn_bwd_workspace", rows, bn.c)), device=xc.device, dtype=torch.uint8)
+        call("avt_bn_bwd", P(g), P(y), P(xc), P(stats[2]), P(stats[3]), P(store.param(bn.prefix + ".weight")),
+             P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc), P(gmask_out), P(ws),
+             rows, bn.c, stream_ptr())
+        return gc
+
+    def _wgrad(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
+        dw = store.grad(spec.name)
+        ev = ConvProfiler.begin()
+        call("avt_conv2d_wgrad", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+             spec.stride, spec.pad, stream_ptr())
+        ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin)
+
+    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None):
+        _, wt = store.packed(spec)
+        gx = torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
+        ev = ConvProfiler.begin()
+        call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
+             spec.stride, spec.pad, stream_ptr())
+        ConvProfiler.end(ev, "dgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin)
+        return gx
+
+    def backward(self, tape: Dict, g_out: torch.Tensor, store: Store):
+        N = tape["N"]
+        g = g_out
+        for blk, t in zip(reversed(self.blocks), reversed(tape["blocks"])):
+            Hc, Wc, Ho, Wo = t["H"], t["W"], t["Ho"], t["Wo"]
+            identity = blk["down"] is None
+            gsum = torch.empty_like(t["c2"]) if identity else None
+            g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gsum)
+            self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
+            g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store)
+            g_c1 = self._bn_bwd(g_h1, t["h1"], t["c1"], t["s1"], blk["bn1"], store)
+            self._wgrad(t["x"], g_c1, N, Hc, Wc, blk["conv1"], store)
+            if identity:
+                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=gsum)
+            else:
+                g_cd = self._bn_bwd(g, t["out"], t["cd"], t["sd"], blk["bnd"], store)
+                self._wgrad(t["x"], g_cd, N, Hc, Wc, blk["down"], store)
+                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store)
+                g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x)
+            g = g_x
+        # maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)
+        H1, W1 = tape["H1"], tape["W1"]
+        g_h0 = torch.empty_like(tape["h0"])
+        call("avt_maxpool3s2_bwd", P(g), P(tape["idx"]), P(g_h0), N, H1, W1, 64, stream_ptr())
+        g_c0 = self._bn_bwd(g_h0, tape["h0"], tape["c0"], tape["st0"], self.bn1, store)
+        self._wgrad(tape["x"], g_c0, N, tape["H"], tape["W"], self.stem, store)

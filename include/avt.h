@@ -1,0 +1,97 @@
+/* libavt — MI355X (gfx950) C-ABI for the audio-visual hard-way train step.
+ *
+ * Every entry point takes plain device pointers + sizes and a hipStream_t (as void*), launches
+ * asynchronously on that stream, never allocates, never synchronises the host, and returns
+ * AVT_OK (0) or a negative code; avt_last_error() returns a thread-local message.
+ * Buffers are owned by the caller (PyTorch's caching allocator in the Python host).
+ *
+ * Layouts: activations NHWC bf16 (raw uint16 bits); statistics/head fp32;
+ * conv master weights fp32 in OHWI order (== channels_last OIHW parameters).
+ *
+ * Reference interface each entry point replaces (tonymisic/audio-visual-tubes):
+ *   avt_conv2d_fwd/dgrad/wgrad   nn.Conv2d fwd + autograd bwd of conv3x3/conv1x1/stems
+ *                                (models/base_models.py:23-30, 135-138; called at 53-69, 195-210)
+ *   avt_bn_finalize/apply/bwd    nn.BatchNorm2d train mode + nn.ReLU(inplace) + residual add
+ *                                (models/base_models.py:39, 46-49, 58-67, 120-121, 141)
+ *   avt_maxpool3s2_fwd/bwd       nn.MaxPool2d(3, 2, 1) (models/base_models.py:143, 203)
+ *   avt_audio_pool_norm_fwd/bwd  nn.AdaptiveMaxPool2d((1,1)) + F.normalize(dim=1) (model.py:96, 120-122)
+ *   avt_hardway_fwd/bwd          AVENet.forward head: normalize, A/A0 einsums, sigmoid trimap,
+ *                                sim1/sim/sim2, logits/0.07, weighted_A (model.py:114-154);
+ *                                HardWayAttention.forward (model.py:46-60)
+ *   avt_hardway_ce               nn.CrossEntropyLoss()(logits, zeros) (train_hardway_1frame.py:113, 130-131)
+ *   avt_adam_step                torch.optim.Adam(lr, weight_decay) step (train_hardway_1frame.py:116, 134)
+ */
+#ifndef AVT_H_
+#define AVT_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVT_OK 0
+#define AVT_EINVAL -1
+#define AVT_EHIP -2
+
+const char* avt_last_error(void);
+int avt_abi_version(void);
+
+/* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
+/* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_partial != NULL also writes per-128-row
+ * tile partials (sum, M2) of the fp32 result: float2[avt_conv2d_fwd_stat_tiles(N,P,Q)][K].
+ * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
+int avt_conv2d_fwd_stat_tiles(int N, int P, int Q);
+int avt_conv2d_fwd(const void* x, const void* wpack, void* y, void* bn_partial, int N, int H, int W, int Cp, int K,
+                   int R, int S, int stride, int pad, int Kg, void* stream);
+/* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
+int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
+                     int R, int S, int stride, int pad, void* stream);
+/* dw[K][R][S][Creal] += wgrad(x[N,H,W,Cp], dy[N,P,Q,K])  (fp32 atomics; caller zeroes dw) */
+int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
+                     int S, int stride, int pad, void* stream);
+
+/* ---- batch norm (train mode) ---- */
+int avt_bn_finalize(const void* partial, int ntiles, int rows, int tile_rows, int C, const float* gamma,
+                    const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                    float* scale, float* shift, float* save_mean, float* save_invstd, void* stream);
+/* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
+int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
+                 const float* rshift, void* out, long long rows, int C, int relu, void* stream);
+int avt_bn_bwd_parts(long long rows, int C);
+size_t avt_bn_bwd_workspace(long long rows, int C);
+/* g' = g*[y>0] (y may be NULL: no mask); dgamma += sum g'*xhat; dbeta += sum g';
+ * gc = gamma*invstd*(g' - mean(g') - xhat*mean(g'*xhat)); gmask_out (optional) = g' */
+int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
+               const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out, void* workspace,
+               long long rows, int C, void* stream);
+
+/* ---- pooling ---- */
+int avt_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, void* stream);
+int avt_maxpool3s2_bwd(const void* gy, const void* idx, void* gx, int N, int H, int W, int C, void* stream);
+int avt_audio_pool_norm_fwd(const void* a, float* an, int* amax, float* anorm, int B, int HW, int C, void* stream);
+int avt_audio_pool_norm_bwd(const float* gan, const float* an, const int* amax, const float* anorm, void* ga, int B,
+                            int HW, int C, void* stream);
+
+/* ---- hard-way head (fp32) ---- */
+size_t avt_hardway_save_floats(int B);
+int avt_hardway_fwd(const void* v, const float* an, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
+                    int use_neg, float* inv, float* vsum, float* A0, float* save, float* logits, float* Aout,
+                    float* Pos, float* Neg, float* wA, void* stream);
+int avt_hardway_ce(const float* logits, int B, int L, float scale, float* loss, float* dlogits, void* stream);
+int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
+                    const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
+                    int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream);
+
+/* ---- optimizer / layout ---- */
+int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
+                  float lr, float beta1, float beta2, float eps, float weight_decay, int step, void* stream);
+int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
+                         void* stream);
+int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream);
+int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AVT_H_ */

@@ -129,6 +129,22 @@ def make_attention_fixture(ref_model, name="hardway_attention_tiny", b=2, t=4, h
     print(f"[{name}] logits[0,:4]={logits[0,:4].tolist()}")
 
 
+TORCH_INIT_PARAMS = ["imgnet.conv1.weight", "imgnet.conv1_a.weight", "imgnet.layer1.0.conv1.weight",
+                     "imgnet.layer4.1.bn2.weight", "audnet.conv1_a.weight", "audnet.layer4.1.conv2.weight",
+                     "audnet.fc.weight", "audnet.fc.bias", "audnet.layer2.0.downsample.0.weight"]
+
+
+def make_torch_init_fixture(ref_model, name="torch_init_seed0"):
+    """The reference's own init under torch.manual_seed(0) (model.py:104-110 after the
+    base_models.py:158-163 init and module construction), as per-tensor checksums."""
+    torch.manual_seed(0)
+    net = ref_model.AVENet(orc.Args(), False)
+    sd = net.state_dict()
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), names=np.array(TORCH_INIT_PARAMS),
+                        checksums=np.stack([checksum(sd[n]) for n in TORCH_INIT_PARAMS]))
+    print(f"[{name}] {len(sd)} entries")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
@@ -136,6 +152,7 @@ def main():
     make_fixture(ref_model, "avenet_tiny_b4", batch=4, img_size=64, freq=65, frames=76)
     make_fixture(ref_model, "avenet_full_b2", batch=2, img_size=224, freq=257, frames=300)
     make_attention_fixture(ref_model)
+    make_torch_init_fixture(ref_model)
 
 
 if __name__ == "__main__":

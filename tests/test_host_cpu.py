@@ -1,0 +1,107 @@
+"""Host-side logic on CPU: the C-ABI library loads and exports every declared symbol, the drop-in
+module tree / state_dict / init match the reference, flat storage aliasing is right, and the
+product path refuses to run without a GPU (no silent CPU fallback)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import avenet_oracle as orc
+from avt_amd import _lib
+from avt_amd.engine import FlatStore, trainable
+from avt_amd.model import AVENet
+from gen_golden import checksum
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(REPO, "include", "avt.h")).read()
+    return sorted(set(re.findall(r"\b(avt_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    lib = _lib.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+        assert s in _lib.SIGNATURES, f"{s} declared in avt.h but not bound in _lib.SIGNATURES"
+    assert lib.avt_abi_version() == 1
+    # pure host queries need no GPU
+    assert _lib.query("avt_conv2d_fwd_stat_tiles", 2, 14, 14) == 4
+    assert _lib.query("avt_hardway_save_floats", 8) == 8 * 20
+
+
+def test_error_path_reports_message():
+    # invalid shape is rejected on the host before any launch
+    with pytest.raises(RuntimeError, match="null pointer"):
+        _lib.call("avt_conv2d_fwd", None, None, None, None, 1, 8, 8, 64, 48, 3, 3, 1, 1, 576, None)
+
+
+def test_state_dict_keys_shapes_match_reference_inventory():
+    m = AVENet(orc.Args(), False)
+    sd = m.state_dict()
+    ref = orc.avenet_entries()
+    assert list(sd.keys()) == [n for n, _, _ in ref]
+    for n, shape, _ in ref:
+        assert tuple(sd[n].shape) == tuple(shape), n
+    assert sum(p.numel() for p in m.parameters()) == 23_422_928
+    assert m._flat.n_train == 22_346_752
+    assert sum(1 for n, _ in m.named_parameters() if trainable(n)) == len(orc.trainable_names(orc.make_state(0)))
+
+
+def test_torch_seeded_init_matches_reference(golden_dir):
+    g = np.load(os.path.join(golden_dir, "torch_init_seed0.npz"), allow_pickle=False)
+    torch.manual_seed(0)
+    m = AVENet(orc.Args(), False)
+    sd = m.state_dict()
+    for n, cs in zip(g["names"], g["checksums"]):
+        np.testing.assert_allclose(checksum(sd[str(n)]), cs, rtol=1e-6, err_msg=str(n))
+
+
+def test_flat_views_alias_storage_and_load_state_dict():
+    m = AVENet(orc.Args(), False)
+    ref = orc.make_state(0)
+    m.load_state_dict(ref)
+    w = m.imgnet.layer2[0].conv1.weight
+    assert w.is_contiguous(memory_format=torch.channels_last)
+    raw = m._flat.raw("imgnet.layer2.0.conv1.weight")
+    assert raw.data_ptr() == w.data_ptr()
+    assert torch.equal(raw.permute(0, 3, 1, 2), ref["imgnet.layer2.0.conv1.weight"])
+    # in-place update through the flat buffer is visible through the parameter
+    m._flat.flat[m._flat.poff["imgnet.layer2.0.conv1.weight"][0]] = 123.0
+    assert w[0, 0, 0, 0].item() == 123.0
+    rm = m.audnet.layer3[1].bn2.running_var
+    assert rm.data_ptr() == m._flat.rawbuf("audnet.layer3.1.bn2.running_var").data_ptr()
+    # trainable parameters occupy the front of the flat buffer
+    offs = [m._flat.poff[n][0] for n in m._flat.pnames if trainable(n)]
+    assert max(offs) < m._flat.n_train
+    assert min(m._flat.poff[n][0] for n in m._flat.pnames if not trainable(n)) >= m._flat.n_train
+
+
+def test_apply_rebinds_views():
+    m = AVENet(orc.Args(), False)
+    m = m.to(torch.device("cpu"))  # _apply path keeps aliasing
+    assert m.imgnet.conv1.weight.data_ptr() == m._flat.raw("imgnet.conv1.weight").data_ptr()
+    with pytest.raises(TypeError):
+        m.double()
+
+
+def test_no_cpu_fallback():
+    m = AVENet(orc.Args(), False)
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(torch.zeros(1, 3, 64, 64), torch.zeros(1, 1, 65, 76))
+
+
+def test_grad_views_layout():
+    m = AVENet(orc.Args(), False)
+    g = torch.arange(m._flat.n_train, dtype=torch.float32)
+    views = m._flat.param_grad_views(g)
+    p = dict(m.named_parameters())
+    for n, v in views.items():
+        assert v.shape == p[n].shape and v.stride() == p[n].stride(), n

@@ -1,0 +1,348 @@
+"""Per-op parity of the libavt HIP kernels (called through the C-ABI) against fp64 CPU
+references of the same op on the same (bf16-rounded) inputs."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from avt_amd._lib import call, query  # noqa: E402
+
+
+def P(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def conv_out(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+def pack(w_ohwi, cp, kg, with_t=True):
+    K, R, S_, C = w_ohwi.shape
+    wf = torch.empty(K, kg, device=DEV, dtype=torch.bfloat16)
+    wt = torch.empty(C, R * S_ * K, device=DEV, dtype=torch.bfloat16) if with_t else None
+    call("avt_pack_conv_weight", P(w_ohwi), K, R, S_, C, cp, kg, P(wf), P(wt), S())
+    return wf, wt
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (2, 9, 11, 64, 64, 3, 1, 1),
+    (2, 9, 11, 64, 128, 3, 2, 1),
+    (3, 7, 5, 128, 256, 1, 2, 0),
+    (2, 5, 6, 256, 512, 3, 1, 1),
+    (1, 17, 19, 512, 512, 3, 1, 1),
+    (2, 15, 13, 64, 128, 1, 2, 0),
+]
+
+
+def _rand_act(N, H, W, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(N, H, W, C, generator=g).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_and_bn_partials(case):
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 1).relu()
+    g = torch.Generator().manual_seed(2)
+    w = (torch.randn(K, R, R, C, generator=g) * (2.0 / (K * R * R)) ** 0.5).float()
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    kg = R * R * C
+    wf, _ = pack(w.to(DEV), C, kg, with_t=False)
+    xd = x.to(DEV)
+    y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
+    tiles = query("avt_conv2d_fwd_stat_tiles", N, Pq, Qq)
+    part = torch.empty(tiles, K, 2, device=DEV)
+    call("avt_conv2d_fwd", P(xd), P(wf), P(y), P(part), N, H, W, C, K, R, R, st, pad, kg, S())
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.to(torch.bfloat16).double().permute(0, 3, 1, 2), stride=st,
+                   padding=pad).permute(0, 2, 3, 1)
+    assert rel_err(y, ref) < 8e-3
+    rows = ref.reshape(-1, K)
+    for t in range(tiles):
+        blk = rows[t * 128:(t + 1) * 128]
+        s = blk.sum(0)
+        m2 = ((blk - blk.mean(0)) ** 2).sum(0)
+        np.testing.assert_allclose(part[t, :, 0].double().cpu().numpy(), s.numpy(), rtol=1e-3, atol=1e-3 * blk.abs().max().item())
+        np.testing.assert_allclose(part[t, :, 1].double().cpu().numpy(), m2.numpy(), rtol=2e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
+def test_stem_fwd_wgrad(cin, cp, H, W):
+    N, K, R, st, pad = 2, 64, 7, 2, 3
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, cin, H, W, generator=g)
+    xd = x.to(DEV)
+    xn = torch.empty(N, H, W, cp, device=DEV, dtype=torch.bfloat16)
+    call("avt_nchw_to_nhwc_bf16", P(xd), P(xn), N, cin, H, W, cp, S())
+    w = (torch.randn(K, R, R, cin, generator=g) * 0.05).float()
+    kg = (R * R * cp + 31) // 32 * 32
+    wf, _ = pack(w.to(DEV), cp, kg, with_t=False)
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
+    call("avt_conv2d_fwd", P(xn), P(wf), P(y), None, N, H, W, cp, K, R, R, st, pad, kg, S())
+    xb = x.to(torch.bfloat16).double()
+    wb = w.to(torch.bfloat16).double().permute(0, 3, 1, 2)
+    ref = F.conv2d(xb, wb, stride=st, padding=pad).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(xn[..., :cin].float().cpu(), x.to(torch.bfloat16).permute(0, 2, 3, 1).float())
+    assert rel_err(y, ref) < 8e-3
+    dy = _rand_act(N, Pq, Qq, K, 4)
+    dw = torch.zeros(K, R, R, cin, device=DEV)
+    call("avt_conv2d_wgrad", P(xn), P(dy.to(DEV)), P(dw), N, H, W, cp, cin, K, R, R, st, pad, S())
+    ref_dw = torch.nn.grad.conv2d_weight(xb, (K, cin, R, R), dy.double().permute(0, 3, 1, 2), stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), ref_dw) < 2e-4
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad(case):
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    dy = _rand_act(N, Pq, Qq, K, 5)
+    g = torch.Generator().manual_seed(6)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float()
+    _, wt = pack(w.to(DEV), C, R * R * C)
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    call("avt_conv2d_dgrad", P(dy.to(DEV)), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.to(torch.bfloat16).double().permute(0, 3, 1, 2),
+                                     dy.double().permute(0, 3, 1, 2), stride=st, padding=pad).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert rel_err(dx, ref) < 8e-3
+    # accumulate path: dx2 = dgrad + add
+    add = _rand_act(N, H, W, C, 7)
+    dx2 = torch.empty_like(dx)
+    call("avt_conv2d_dgrad", P(dy.to(DEV)), P(wt), P(dx2), P(add.to(DEV)), N, H, W, C, K, R, R, st, pad, S())
+    torch.cuda.synchronize()
+    assert rel_err(dx2, ref + add.double()) < 8e-3
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wgrad(case):
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    x = _rand_act(N, H, W, C, 8).relu()
+    dy = _rand_act(N, Pq, Qq, K, 9)
+    dw = torch.zeros(K, R, R, C, device=DEV)
+    call("avt_conv2d_wgrad", P(x.to(DEV)), P(dy.to(DEV)), P(dw), N, H, W, C, C, K, R, R, st, pad, S())
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), ref) < 2e-4
+
+
+def test_wgrad_large_splitk():
+    # many pixels -> split-K with fp32 atomics
+    N, H, W, C, K, R, st, pad = 8, 56, 56, 64, 64, 3, 1, 1
+    x = _rand_act(N, H, W, C, 10).relu()
+    dy = _rand_act(N, H, W, K, 11)
+    dw = torch.zeros(K, R, R, C, device=DEV)
+    call("avt_conv2d_wgrad", P(x.to(DEV)), P(dy.to(DEV)), P(dw), N, H, W, C, C, K, R, R, st, pad, S())
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
+                                      stride=st, padding=pad)
+    torch.cuda.synchronize()
+    assert rel_err(dw.permute(0, 3, 1, 2), ref) < 2e-4
+
+
+# ------------------------------------------------------------------------------------------ BN
+def _tile_partials(c):
+    rows = c.double().reshape(-1, c.shape[-1])
+    parts = []
+    for t in range(0, rows.shape[0], 128):
+        blk = rows[t:t + 128]
+        parts.append(torch.stack([blk.sum(0), ((blk - blk.mean(0)) ** 2).sum(0)], -1))
+    return torch.stack(parts).float()
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128)])
+def test_bn_forward_train(shape):
+    N, H, W, C = shape
+    c = (_rand_act(N, H, W, C, 12).float() * 1.7 + 0.3).to(torch.bfloat16)
+    res = _rand_act(N, H, W, C, 13)
+    g = torch.Generator().manual_seed(14)
+    gamma = 1 + 0.02 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    part = _tile_partials(c).to(DEV)
+    stats = torch.empty(4, C, device=DEV)
+    rmd, rvd = rm.to(DEV), rv.to(DEV)
+    rows = N * H * W
+    call("avt_bn_finalize", P(part), part.shape[0], rows, 128, C, P(gamma.to(DEV)), P(beta.to(DEV)), P(rmd), P(rvd),
+         ctypes.c_float(0.1), ctypes.c_float(1e-5), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
+    out = torch.empty_like(c, device=DEV)
+    call("avt_bn_apply", P(c.to(DEV)), P(stats[0]), P(stats[1]), P(res.to(DEV)), None, None, P(out), rows, C, 1, S())
+    torch.cuda.synchronize()
+    cn = c.double().permute(0, 3, 1, 2)
+    rm64, rv64 = rm.double(), rv.double()
+    ref = F.batch_norm(cn, rm64, rv64, gamma.double(), beta.double(), True, 0.1, 1e-5)
+    ref = (ref + res.double().permute(0, 3, 1, 2)).relu().permute(0, 2, 3, 1)
+    assert rel_err(out, ref) < 8e-3
+    np.testing.assert_allclose(rmd.cpu().numpy(), rm64.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(rvd.cpu().numpy(), rv64.numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128)])
+@pytest.mark.parametrize("masked", [True, False])
+def test_bn_backward(shape, masked):
+    N, H, W, C = shape
+    c = (_rand_act(N, H, W, C, 15).float() * 1.3 - 0.2).to(torch.bfloat16)
+    gy = _rand_act(N, H, W, C, 16)
+    g = torch.Generator().manual_seed(17)
+    gamma = 1 + 0.02 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
+    gm = gamma.double().requires_grad_(True)
+    bt = beta.double().requires_grad_(True)
+    yb = F.batch_norm(cn, None, None, gm, bt, True, 0.1, 1e-5)
+    y = yb.relu() if masked else yb
+    y.backward(gy.double().permute(0, 3, 1, 2))
+    mean = c.double().reshape(-1, C).mean(0)
+    var = c.double().reshape(-1, C).var(0, unbiased=False)
+    inv = (var + 1e-5).rsqrt()
+    yd = y.detach().permute(0, 2, 3, 1).to(torch.bfloat16).to(DEV).contiguous()
+    rows = N * H * W
+    ws = torch.empty(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
+    dgamma = torch.zeros(C, device=DEV)
+    dbeta = torch.zeros(C, device=DEV)
+    gc = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    gmask = torch.empty_like(gc)
+    call("avt_bn_bwd", P(gy.to(DEV)), P(yd if masked else None), P(c.to(DEV)), P(mean.float().to(DEV)),
+         P(inv.float().to(DEV)), P(gamma.to(DEV)), P(dgamma), P(dbeta), P(gc), P(gmask), P(ws), rows, C, S())
+    torch.cuda.synchronize()
+    assert rel_err(gc, cn.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(dgamma, gm.grad) < 1e-2
+    assert rel_err(dbeta, bt.grad) < 1e-3
+
+
+# ------------------------------------------------------------------------------------------ pools
+@pytest.mark.parametrize("shape", [(2, 12, 14, 64), (2, 129, 150, 64), (1, 7, 9, 64)])
+def test_maxpool(shape):
+    N, H, W, C = shape
+    x = _rand_act(N, H, W, C, 18).relu()  # post-ReLU, many ties at 0 like the stem
+    P2, Q2 = conv_out(H, 3, 2, 1), conv_out(W, 3, 2, 1)
+    y = torch.empty(N, P2, Q2, C, device=DEV, dtype=torch.bfloat16)
+    idx = torch.empty(N, P2, Q2, C, device=DEV, dtype=torch.uint8)
+    xd = x.to(DEV)
+    call("avt_maxpool3s2_fwd", P(xd), P(y), P(idx), N, H, W, C, S())
+    gy = _rand_act(N, P2, Q2, C, 19)
+    gx = torch.empty_like(xd)
+    call("avt_maxpool3s2_bwd", P(gy.to(DEV)), P(idx), P(gx), N, H, W, C, S())
+    xn = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xn, 3, 2, 1)
+    yr.backward(gy.double().permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu().double(), yr.detach().permute(0, 2, 3, 1))
+    # gradients: exact except where a window has tied maxima (routing may differ); ties only at 0
+    # here and those positions are masked by the ReLU backward in the real network.
+    ref = xn.grad.permute(0, 2, 3, 1)
+    nz = x.double() > 0
+    assert rel_err(gx.cpu().double() * nz, ref * nz) < 8e-3
+
+
+@pytest.mark.parametrize("B,HW,C", [(3, 323, 512), (5, 25, 512), (2, 7, 64)])
+def test_audio_pool_norm(B, HW, C):
+    a = _rand_act(B, HW, 1, C, 20).reshape(B, HW, C)
+    an = torch.empty(B, C, device=DEV)
+    amax = torch.empty(B, C, device=DEV, dtype=torch.int32)
+    anorm = torch.empty(B, device=DEV)
+    ad = a.to(DEV)
+    call("avt_audio_pool_norm_fwd", P(ad), P(an), P(amax), P(anorm), B, HW, C, S())
+    g = torch.Generator().manual_seed(21)
+    gan = torch.randn(B, C, generator=g)
+    ga = torch.empty_like(ad)
+    call("avt_audio_pool_norm_bwd", P(gan.to(DEV)), P(an), P(amax), P(anorm), P(ga), B, HW, C, S())
+    at = a.double().permute(0, 2, 1).reshape(B, C, HW, 1).requires_grad_(True)
+    r = F.normalize(F.adaptive_max_pool2d(at, 1).flatten(1), dim=1)
+    r.backward(gan.double())
+    torch.cuda.synchronize()
+    assert rel_err(an, r.detach()) < 1e-6
+    assert rel_err(ga, at.grad.reshape(B, C, HW).permute(0, 2, 1)) < 8e-3
+
+
+# ------------------------------------------------------------------------------------------ head
+def _head_inputs(B, h, w, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    v = (torch.randn(B, h, w, C, generator=g).abs() + 0.3 * torch.rand(B, 1, 1, C, generator=g)).to(torch.bfloat16)
+    an = F.normalize(torch.randn(B, C, generator=g).abs() + 0.5, dim=1)
+    return v, an
+
+
+@pytest.mark.parametrize("B,h,w,trimap,neg", [(2, 14, 14, True, True), (8, 14, 14, True, True), (5, 4, 4, False, True),
+                                           (3, 7, 9, True, False), (40, 14, 14, True, True)])
+def test_hardway_head(B, h, w, trimap, neg):
+    import avenet_oracle as orc
+
+    C = 512
+    v, an = _head_inputs(B, h, w, C, 22)
+    Pn = h * w
+    dev = dict(device=DEV, dtype=torch.float32)
+    L = B + (2 if neg else 1)
+    inv, vsum = torch.empty(B, Pn, **dev), torch.empty(B, Pn, **dev)
+    A0 = torch.empty(B, Pn, B, **dev)
+    save = torch.empty(int(query("avt_hardway_save_floats", B)), **dev)
+    logits, A, Pos, Neg, wA = (torch.empty(B, L, **dev), torch.empty(B, Pn, **dev), torch.empty(B, Pn, **dev),
+                               torch.empty(B, Pn, **dev), torch.empty(B, Pn, **dev))
+    vd, and_ = v.to(DEV), an.to(DEV)
+    call("avt_hardway_fwd", P(vd), P(and_), B, Pn, C, 0.65, 0.4, 0.03, int(trimap), int(neg), P(inv), P(vsum), P(A0),
+         P(save), P(logits), P(A), P(Pos), P(Neg), P(wA), S())
+    loss = torch.empty((), **dev)
+    dl = torch.empty(B, L, **dev)
+    call("avt_hardway_ce", P(logits), B, L, 1.0, P(loss), P(dl), S())
+    dA0 = torch.empty(B, Pn, B, **dev)
+    dvh = torch.empty(B, Pn, C, **dev)
+    gv = torch.empty_like(vd)
+    gan = torch.empty(B, C, **dev)
+    call("avt_hardway_bwd", P(vd), P(and_), P(inv), P(A0), P(save), P(dl), B, Pn, C, 0.65, 0.4, 0.03, int(trimap),
+         int(neg), P(dA0), P(dvh), P(gv), P(gan), S())
+    torch.cuda.synchronize()
+    # fp64 oracle on the same (bf16) features
+    vt = v.double().permute(0, 3, 1, 2).requires_grad_(True)
+    at = an.double().requires_grad_(True)
+    img_n = F.normalize(vt, dim=1)
+    rA, rlog, rwA, rPos, rNeg = orc.hardway_head(img_n, at, 0.65, 0.4, 0.03, trimap, neg)
+    rloss = orc.hardway_ce(rlog)
+    rloss.backward()
+    assert (A.cpu().double() - rA.detach().reshape(B, Pn)).abs().max() < 1e-5
+    assert (logits.cpu().double() - rlog.detach()).abs().max() < 2e-3
+    assert abs(loss.item() - rloss.item()) < 1e-5 * max(1.0, abs(rloss.item()))
+    assert (Pos.cpu().double() - rPos.detach().reshape(B, Pn)).abs().max() < 1e-3
+    assert (Neg.cpu().double() - rNeg.detach().reshape(B, Pn)).abs().max() < 1e-3
+    assert (wA.cpu().double() - rwA.detach().reshape(B, Pn)).abs().max() < 1e-5
+    assert rel_err(gan, at.grad) < 2e-3
+    assert rel_err(gv, vt.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_adam_matches_torch():
+    import avenet_oracle as orc
+
+    g = torch.Generator().manual_seed(23)
+    n = 1001
+    p0 = torch.randn(n, generator=g)
+    opt = orc.AdamRef(lr=1e-3, weight_decay=1e-4)
+    pr = {"p": p0.clone().double()}
+    pd = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for t in range(1, 4):
+        gr = torch.randn(n, generator=g)
+        opt.step(pr, {"p": gr.double()})
+        call("avt_adam_step", P(pd), P(gr.to(DEV)), P(m), P(v), n, 1.0, 1e-3, 0.9, 0.999, 1e-8, 1e-4, t, S())
+    torch.cuda.synchronize()
+    assert rel_err(pd - p0.to(DEV), pr["p"] - p0.double()) < 1e-4
