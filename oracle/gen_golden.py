@@ -65,6 +65,50 @@ def run_reference(ref_model, sd, image, audio, dtype):
                 after=after, bufs=bufs)
 
 
+def run_reference_bf16_trunks(ref_model, sd, image, audio):
+    """The reference's own trunks (net.imgnet / net.audnet, base_models.py:195-210) under CPU bf16
+    autocast, with the fp32 head (model.py:116-154, restated bit-exactly by avenet_oracle) —
+    the SURVEY §0.7 "bf16 backbone, fp32 similarity math" configuration.  Its deviation from the
+    fp64 run is the yardstick for any bf16-trunk implementation's tolerances."""
+    net = ref_model.AVENet(orc.Args(), False)
+    net.load_state_dict(sd, strict=True)
+    net.train()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        img = net.imgnet(image)
+        aud = net.audnet(audio)
+    img = torch.nn.functional.normalize(img.float(), dim=1)
+    aud = torch.nn.functional.normalize(torch.nn.functional.adaptive_max_pool2d(aud.float(), 1).flatten(1), dim=1)
+    A, logits, wA, Pos, Neg = orc.hardway_head(img, aud)
+    loss = torch.nn.CrossEntropyLoss()(logits, torch.zeros(logits.shape[0], dtype=torch.long))
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+    return dict(A=A.detach(), logits=logits.detach(), weighted_A=wA.detach(), loss=loss.detach(), grads=grads)
+
+
+def deviation(res, r64, names, b):
+    """Deviation metrics of a run from the fp64 reference (same metrics the GPU tests assert)."""
+    off = ~np.eye(b, b + 2, k=1, dtype=bool)
+    diag = np.eye(b, b + 2, k=1, dtype=bool)
+    lg, l64 = res["logits"].double().numpy(), r64["logits"].numpy()
+    gn = np.array([res["grads"][n].double().norm().item() for n in names])
+    g64 = np.array([r64["grads"][n].norm().item() for n in names])
+    cos = []
+    for n in SLICE_PARAMS:
+        a = res["grads"][n].double().flatten()[:64].numpy()
+        r = r64["grads"][n].flatten()[:64].numpy()
+        cos.append(float(a @ r / (np.linalg.norm(a) * np.linalg.norm(r))))
+    return {
+        "A_abs": np.abs(res["A"].double().numpy() - r64["A"].numpy()).max(),
+        "logits_off_abs": np.abs(lg[off] - l64[off]).max(),
+        "logits_diag_rel": (np.abs(lg[diag] - l64[diag]) / np.abs(l64[diag])).max(),
+        "loss_rel": abs(res["loss"].item() - r64["loss"].item()) / abs(r64["loss"].item()),
+        "wA_rel": np.abs(res["weighted_A"].double().numpy() - r64["weighted_A"].numpy()).max()
+        / np.abs(r64["weighted_A"].numpy()).max(),
+        "gradnorm_rel": np.abs(gn - g64) / g64,
+        "slice_cos": np.array(cos),
+    }
+
+
 SLICE_PARAMS = [
     "imgnet.conv1.weight", "audnet.conv1_a.weight", "imgnet.layer1.0.conv1.weight",
     "imgnet.layer2.0.downsample.0.weight", "imgnet.layer4.1.conv2.weight",
@@ -96,6 +140,11 @@ def make_fixture(ref_model, name, batch, img_size, freq, frames, seed_w=0):
         out["delta_slice_f64/" + n] = (r64["after"][n] - r64["before"][n]).flatten()[:64].numpy()
     for n in BUF_SLICES:
         out["buf_f64/" + n] = r64["bufs"][n][:16].numpy()
+    dev = deviation(run_reference_bf16_trunks(ref_model, sd, image, audio), r64, names, batch)
+    for k, v in dev.items():
+        out["bf16ref_dev/" + k] = np.asarray(v)
+    print(f"[{name}] bf16-trunk reference deviation: " + ", ".join(
+        f"{k}={np.max(v) if k != 'slice_cos' else np.min(v):.3e}" for k, v in dev.items()))
     out["image_checksum"] = checksum(image)
     out["audio_checksum"] = checksum(audio)
     out["weight_checksum"] = np.array([checksum(sd[n])[0] for n in SLICE_PARAMS])

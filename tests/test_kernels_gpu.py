@@ -12,8 +12,22 @@ pytestmark = pytest.mark.gpu
 from avt_amd._lib import call, query  # noqa: E402
 
 
+_KEEP = []  # device temporaries passed to the C-ABI stay alive until the test ends
+
+
+@pytest.fixture(autouse=True)
+def _keep_alive():
+    yield
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    _KEEP.clear()
+
+
 def P(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    if t is None:
+        return None
+    _KEEP.append(t)
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def S():
