@@ -26,13 +26,13 @@ _Z = ctypes.c_size_t
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
     "avt_abi_version": (_I, []),
-    "avt_conv2d_fwd_stat_tiles": (_I, [_I, _I, _I]),
+    "avt_bn_slots": (_I, []),
+    "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "avt_bn_finalize": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
+    "avt_bn_finalize": (_I, [_P, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
     "avt_bn_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P]),
-    "avt_bn_bwd_parts": (_I, [_L, _I]),
     "avt_bn_bwd_workspace": (_Z, [_L, _I]),
     "avt_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "avt_maxpool3s2_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
@@ -45,6 +45,8 @@ SIGNATURES = {
     "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "avt_pack_desc_bytes": (_Z, []),
+    "avt_pack_conv_weights_batched": (_I, [_P, _I, _L, _P]),
     "avt_nchw_to_nhwc_bf16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "avt_nhwc_bf16_to_nchw": (_I, [_P, _P, _I, _I, _I, _P]),
 }

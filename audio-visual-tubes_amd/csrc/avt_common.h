@@ -16,6 +16,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define AVT_OK 0
 #define AVT_EINVAL -1
 #define AVT_EHIP -2
+#define AVT_BN_SLOTS 16  // spread of the fp64 BN statistic accumulators (atomic contention)
 
 namespace avt {
 

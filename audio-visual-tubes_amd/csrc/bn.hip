@@ -1,12 +1,15 @@
 // Train-mode BatchNorm2d (+ReLU, +residual) for the ResNet-18 trunks, NHWC bf16 activations,
-// fp32 statistics.  Semantics of torch BatchNorm2d as used at models/base_models.py:39,46-49,
-// 120-121,141 (eps 1e-5, momentum 0.1): normalise with the biased batch variance, update
-// running_var with the unbiased one.
+// fp32 math, fp64 statistic accumulation.  Semantics of torch BatchNorm2d as used at
+// models/base_models.py:39,46-49,120-121,141 (eps 1e-5, momentum 0.1): normalise with the biased
+// batch variance, update running_var with the unbiased one.
 //
-//   fwd : stats come from the conv epilogue as per-128-row tile partials (sum, M2 about the tile
-//         mean) -> bn_finalize (Chan merge) -> scale/shift -> bn_apply (+residual, +ReLU).
-//   bwd : bn_bwd_reduce (sum g', sum g'*xhat per block, g' = g*[y>0]) -> bn_bwd_finalize
-//         (dgamma, dbeta, k1, k2) -> bn_bwd_apply: g_c = gamma*invstd*(g' - k1 - xhat*k2).
+//   fwd : the conv epilogue adds per-128-row-tile (sum_t, M2_t, sum_t^2/n_t) into an fp64
+//         accumulator [AVT_BN_SLOTS][C][3]; bn_finalize merges the slots exactly
+//         (M2 = sum M2_t + sum sum_t^2/n_t - S^2/N, Chan's formula), writes scale/shift/mean/invstd,
+//         updates running stats and re-zeroes the accumulator; bn_apply (+residual, +ReLU).
+//   bwd : bn_bwd_reduce adds per-block (sum g', sum g'*xhat) (g' = g*[y>0]) into an fp64
+//         accumulator [AVT_BN_SLOTS][C][2] -> bn_bwd_finalize (dgamma, dbeta, k1, k2; re-zeroes) ->
+//         bn_bwd_apply: g_c = gamma*invstd*(g' - k1 - xhat*k2).
 #include "avt_common.h"
 
 namespace avt {
@@ -28,53 +31,40 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// Chan et al. parallel merge of (n, mean, M2)
-__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
-  if (nb <= 0.f) return;
-  const float nn = n + nb;
-  const float d = meanb - mean;
-  const float f = nb / nn;
-  mean += d * f;
-  m2 += m2b + d * d * n * f;
-  n = nn;
-}
-
-// one block = 64 channels x 16 tile-rows (1024 threads)
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float2* __restrict__ part, int ntiles, int rows,
-                                                           int tile_rows, int C, const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float* running_mean,
-                                                           float* running_var, float momentum, float eps,
-                                                           float* scale, float* shift, float* save_mean,
-                                                           float* save_invstd) {
-  __shared__ float sn[16][64], sm[16][64], s2[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C) {
-    for (int t = ty; t < ntiles; t += 16) {
-      const float2 pr = part[(size_t)t * C + c];
-      const float nt = (float)min(tile_rows, rows - t * tile_rows);
-      chan_merge(n, mean, m2, nt, pr.x / nt, pr.y);
-    }
+// one thread per channel
+__global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, float momentum, float eps, float* scale,
+                                                          float* shift, float* save_mean, float* save_invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0, R = 0.0;
+#pragma unroll
+  for (int s = 0; s < AVT_BN_SLOTS; ++s) {
+    double* a = acc + ((size_t)s * C + c) * 3;
+    S += a[0];
+    Q += a[1];
+    R += a[2];
+    a[0] = 0.0;
+    a[1] = 0.0;
+    a[2] = 0.0;
   }
-  sn[ty][tx] = n;
-  sm[ty][tx] = mean;
-  s2[ty][tx] = m2;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    for (int k = 1; k < 16; ++k) chan_merge(n, mean, m2, sn[k][tx], sm[k][tx], s2[k][tx]);
-    const float var = m2 / n;
-    const float inv = rsqrtf(var + eps);
-    const float sc = gamma[c] * inv;
-    scale[c] = sc;
-    shift[c] = beta[c] - mean * sc;
-    if (save_mean) save_mean[c] = mean;
-    if (save_invstd) save_invstd[c] = inv;
-    if (running_mean) {
-      const float unb = n > 1.f ? m2 / (n - 1.f) : var;
-      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
-    }
+  const double n = (double)rows;
+  const double mean = S / n;
+  double m2 = Q + (R - S * mean);
+  if (m2 < 0.0) m2 = 0.0;
+  const float var = (float)(m2 / n);
+  const float inv = rsqrtf(var + eps);
+  const float sc = gamma[c] * inv;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  if (save_mean) save_mean[c] = (float)mean;
+  if (save_invstd) save_invstd[c] = inv;
+  if (running_mean) {
+    const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
   }
 }
 
@@ -110,13 +100,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// Per-block partial sums of g' and g'*xhat.  Block: 256 threads; thread owns channel chunk
-// (tid % (C/8)) and walks rows tid/(C/8) + k*(256/(C/8)) of the block's row range.
+// Per-block sums of g' and g'*xhat added into acc[block % SLOTS][C][2].  Block: 256 threads; a
+// thread owns channel chunk (tid % (C/8)) and walks rows tid/(C/8) + k*(256/(C/8)).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                                             const bf16_t* __restrict__ xc, const float* __restrict__ mean,
-                                                            const float* __restrict__ invstd, float2* __restrict__ part,
-                                                            int rows, int C, int rows_per_block) {
-  extern __shared__ float red[];  // [256/(C/8)][C][2]
+                                                            const float* __restrict__ invstd, double* __restrict__ acc,
+                                                            long long rows, int C, int rows_per_block) {
+  __shared__ float red[2048 * 2];  // [256/(C/8)][C][2] = 4096 floats for any C
   const int cv = C / 8;
   const int chunk = threadIdx.x % cv, r0 = threadIdx.x / cv, rstep = 256 / cv;
   const int c0 = chunk * 8;
@@ -128,72 +118,61 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     s1[e] = 0.f;
     s2[e] = 0.f;
   }
-  const int rbeg = blockIdx.x * rows_per_block, rend = min(rows, rbeg + rows_per_block);
-  if (r0 < rstep) {
-    for (int r = rbeg + r0; r < rend; r += rstep) {
-      const size_t off = (size_t)r * cv + chunk;
-      float gg[8], xx[8];
-      unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
-      unpack8(reinterpret_cast<const u32x4*>(xc)[off], xx);
-      if (y) {
-        float yy[8];
-        unpack8(reinterpret_cast<const u32x4*>(y)[off], yy);
+  const long long rbeg = (long long)blockIdx.x * rows_per_block;
+  const long long rend = min(rows, rbeg + rows_per_block);
+  for (long long r = rbeg + r0; r < rend; r += rstep) {
+    const size_t off = (size_t)r * cv + chunk;
+    float gg[8], xx[8];
+    unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
+    unpack8(reinterpret_cast<const u32x4*>(xc)[off], xx);
+    if (y) {
+      float yy[8];
+      unpack8(reinterpret_cast<const u32x4*>(y)[off], yy);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += gg[e];
-        s2[e] += gg[e] * (xx[e] - mu[e]) * is[e];
-      }
+      for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
     }
-  }
-  const int nr = rstep;  // rows of partials in LDS
-  if (r0 < nr) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[(r0 * C + c0 + e) * 2] = s1[e];
-      red[(r0 * C + c0 + e) * 2 + 1] = s2[e];
+      s1[e] += gg[e];
+      s2[e] += gg[e] * (xx[e] - mu[e]) * is[e];
     }
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(r0 * C + c0 + e) * 2] = s1[e];
+    red[(r0 * C + c0 + e) * 2 + 1] = s2[e];
+  }
   __syncthreads();
+  double* slot = acc + (size_t)(blockIdx.x % AVT_BN_SLOTS) * C * 2;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float a = 0.f, b = 0.f;
-    for (int k = 0; k < nr; ++k) {
+    for (int k = 0; k < rstep; ++k) {
       a += red[(k * C + c) * 2];
       b += red[(k * C + c) * 2 + 1];
     }
-    part[(size_t)blockIdx.x * C + c] = make_float2(a, b);
+    atomicAdd(slot + 2 * c, (double)a);
+    atomicAdd(slot + 2 * c + 1, (double)b);
   }
 }
 
-// Sum block partials; write dgamma/dbeta (accumulated into grads if non-null) and k1,k2.
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float2* __restrict__ part, int nparts, int C,
-                                                               float inv_rows, float* dgamma, float* dbeta, float* k1,
-                                                               float* k2) {
-  __shared__ float sa[16][64], sb[16][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
-  float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int t = ty; t < nparts; t += 16) {
-      const float2 pr = part[(size_t)t * C + c];
-      a += pr.x;
-      b += pr.y;
-    }
-  sa[ty][tx] = a;
-  sb[ty][tx] = b;
-  __syncthreads();
-  if (ty == 0 && c < C) {
-    for (int k = 1; k < 16; ++k) {
-      a += sa[k][tx];
-      b += sb[k][tx];
-    }
-    if (dbeta) dbeta[c] += a;
-    if (dgamma) dgamma[c] += b;
-    k1[c] = a * inv_rows;
-    k2[c] = b * inv_rows;
+// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
+                                                              float* dgamma, float* dbeta, float* k1, float* k2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int s = 0; s < AVT_BN_SLOTS; ++s) {
+    double* p = acc + ((size_t)s * C + c) * 2;
+    a += p[0];
+    b += p[1];
+    p[0] = 0.0;
+    p[1] = 0.0;
   }
+  if (dbeta) dbeta[c] += (float)a;
+  if (dgamma) dgamma[c] += (float)b;
+  k1[c] = (float)(a * inv_rows);
+  k2[c] = (float)(b * inv_rows);
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
@@ -237,14 +216,15 @@ static int ew_grid(long long nvec) {
 
 using namespace avt;
 
-extern "C" int avt_bn_finalize(const void* partial, int ntiles, int rows, int tile_rows, int C, const float* gamma,
-                               const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                               float* scale, float* shift, float* save_mean, float* save_invstd, void* stream) {
-  AVT_REQUIRE(partial && gamma && beta && scale && shift, "bn_finalize: null pointer");
+extern "C" size_t avt_bn_acc_doubles(int C) { return (size_t)AVT_BN_SLOTS * C * 3; }
+
+extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta,
+                               float* running_mean, float* running_var, float momentum, float eps, float* scale,
+                               float* shift, float* save_mean, float* save_invstd, void* stream) {
+  AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream,
-                     (const float2*)partial, ntiles, rows, tile_rows, C, gamma, beta, running_mean, running_var,
-                     momentum, eps, scale, shift, save_mean, save_invstd);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+                     beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
   return check_launch("bn_finalize");
 }
 
@@ -261,35 +241,35 @@ extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shif
   return check_launch("bn_apply");
 }
 
-extern "C" int avt_bn_bwd_parts(long long rows, int C) {
-  const int rows_per_block = 256;
-  return (int)((rows + rows_per_block - 1) / rows_per_block);
+// workspace: AVT_BN_SLOTS*C*2 doubles (must be zero on entry; left zero on exit) + 2*C floats
+extern "C" size_t avt_bn_bwd_workspace(long long rows, int C) {
+  (void)rows;
+  return (size_t)AVT_BN_SLOTS * C * 2 * sizeof(double) + 2 * (size_t)C * sizeof(float);
 }
 
 extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
                           const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out,
                           void* workspace, long long rows, int C, void* stream) {
-  // workspace: avt_bn_bwd_parts(rows,C)*C float2 + 2*C floats
   AVT_REQUIRE(g && xc && mean && invstd && gamma && gc && workspace, "bn_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn_bwd: C=%d unsupported", C);
   AVT_REQUIRE(rows > 0, "bn_bwd: empty input");
-  const int rpb = 256;
-  const int nparts = avt_bn_bwd_parts(rows, C);
-  float2* part = (float2*)workspace;
-  float* k1 = (float*)(part + (size_t)nparts * C);
+  AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_bwd: workspace must be 8-byte aligned");
+  double* acc = (double*)workspace;
+  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  const int nr = 256 / (C / 8);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), nr * C * 2 * sizeof(float), st, (const bf16_t*)g,
-                     (const bf16_t*)y, (const bf16_t*)xc, mean, invstd, part, (int)rows, C, rpb);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, nparts, C,
-                     1.0f / (float)rows, dgamma, dbeta, k1, k2);
+  // ~2 blocks per CU of rows
+  long long rpb = (rows + 511) / 512;
+  const int rstep = 256 / (C / 8);
+  rpb = ((rpb + rstep - 1) / rstep) * rstep;
+  if (rpb < rstep) rpb = rstep;
+  const int nblk = (int)((rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
+                     (const bf16_t*)xc, mean, invstd, acc, rows, C, (int)rpb);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
                      (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc, (bf16_t*)gmask_out, nvec, C);
   return check_launch("bn_bwd");
-}
-
-extern "C" size_t avt_bn_bwd_workspace(long long rows, int C) {
-  return (size_t)avt_bn_bwd_parts(rows, C) * C * sizeof(float) * 2 + 2 * (size_t)C * sizeof(float);
 }

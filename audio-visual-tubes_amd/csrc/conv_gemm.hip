@@ -24,7 +24,9 @@ struct GemmNTParams {
   const bf16_t* wmat;  // [Ng][Kg] bf16, K contiguous
   bf16_t* out;         // [M][Ng] bf16
   const bf16_t* add;   // optional [M][Ng] bf16 added to the result (may alias out)
-  float2* stats;       // optional [ceil(M/BM)][Ng] (sum, M2 about the tile mean) of fp32 results
+  double* stats;       // optional BN accumulator [AVT_BN_SLOTS][Ng][3]: per 128-row tile t the fp32
+                       // results' (sum_t, M2_t about the tile mean, sum_t^2/n_t) are added (fp64
+                       // atomics) into slot t % AVT_BN_SLOTS
   int M, Ng, Kg;
   int IH, IW, IC;      // source tensor geometry
   int OH, OW;          // pixel grid of the GEMM rows
@@ -227,8 +229,14 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
       (void)colsum;
     }
     __syncthreads();
+    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
     for (int c = tid; c < BN; c += 256) {
-      p.stats[(size_t)mt * p.Ng + n0 + c] = make_float2(red[c] + red[BN + c], red[2 * BN + c] + red[3 * BN + c]);
+      const double s = (double)red[c] + (double)red[BN + c];
+      const double m2 = (double)red[2 * BN + c] + (double)red[3 * BN + c];
+      double* a = acc_slot + (size_t)(n0 + c) * 3;
+      atomicAdd(a + 0, s);
+      atomicAdd(a + 1, m2);
+      atomicAdd(a + 2, s * s / (double)rows_valid);
     }
   }
 
@@ -461,9 +469,9 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
   hipLaunchKernelGGL((gemm_nt_kernel<MODE, CVEC, BM, BN>), dim3(grid), dim3(256), 0, st, p);
 }
 
-extern "C" int avt_conv2d_fwd_stat_tiles(int N, int P, int Q) { return (N * P * Q + 127) / 128; }
+extern "C" int avt_bn_slots(void) { return AVT_BN_SLOTS; }
 
-extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, void* bn_partial, int N, int H, int W,
+extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W,
                               int Cp, int K, int R, int S, int stride, int pad, int Kg, void* stream) {
   AVT_REQUIRE(x && wpack && y, "conv2d_fwd: null pointer");
   AVT_REQUIRE(K % 64 == 0, "conv2d_fwd: K=%d must be a multiple of 64", K);
@@ -476,7 +484,7 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, void* b
   p.wmat = (const bf16_t*)wpack;
   p.out = (bf16_t*)y;
   p.add = nullptr;
-  p.stats = (float2*)bn_partial;
+  p.stats = bn_acc;
   p.IH = H; p.IW = W; p.IC = Cp;
   p.OH = conv_out(H, R, stride, pad);
   p.OW = conv_out(W, S, stride, pad);

@@ -193,21 +193,25 @@ __global__ __launch_bounds__(256) void hardway_logits_kernel(const float* __rest
 }
 
 // ---- CE(target 0), mean over the B rows, times `scale`: loss and dlogits ----
-__global__ void hardway_ce_kernel(const float* __restrict__ logits, int B, int L, float scale, float* __restrict__ loss,
-                                  float* __restrict__ dlogits) {
+// one block of 1024 threads; wave w handles rows w, w+16, ... with lane-parallel max/sum
+__global__ __launch_bounds__(1024) void hardway_ce_kernel(const float* __restrict__ logits, int B, int L, float scale,
+                                                          float* __restrict__ loss, float* __restrict__ dlogits) {
   __shared__ float red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float part = 0.f;
-  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+  for (int i = w; i < B; i += 16) {
     const float* r = logits + (size_t)i * L;
     float mx = -INFINITY;
-    for (int j = 0; j < L; ++j) mx = fmaxf(mx, r[j]);
+    for (int j = lane; j < L; j += 64) mx = fmaxf(mx, r[j]);
+    mx = wave_max(mx);
     float se = 0.f;
-    for (int j = 0; j < L; ++j) se += __expf(r[j] - mx);
-    const float lse = mx + __logf(se);
-    part += lse - r[0];
+    for (int j = lane; j < L; j += 64) se += expf(r[j] - mx);
+    se = wave_sum(se);
+    const float lse = mx + logf(se);
+    if (lane == 0) part += lse - r[0];
     if (dlogits) {
-      for (int j = 0; j < L; ++j) {
-        const float sm = __expf(r[j] - lse);
+      for (int j = lane; j < L; j += 64) {
+        const float sm = expf(r[j] - lse);
         dlogits[(size_t)i * L + j] = (sm - (j == 0 ? 1.f : 0.f)) * scale / (float)B;
       }
     }
@@ -324,7 +328,7 @@ extern "C" int avt_hardway_fwd(const void* v, const float* an, int B, int P, int
 extern "C" int avt_hardway_ce(const float* logits, int B, int L, float scale, float* loss, float* dlogits,
                               void* stream) {
   AVT_REQUIRE(logits, "hardway_ce: null pointer");
-  hipLaunchKernelGGL(hardway_ce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, logits, B, L, scale, loss, dlogits);
+  hipLaunchKernelGGL(hardway_ce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, logits, B, L, scale, loss, dlogits);
   return check_launch("hardway_ce");
 }
 

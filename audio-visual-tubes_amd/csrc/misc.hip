@@ -84,6 +84,35 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ w, bf16_t* __restric
   }
 }
 
+// Batched packing of many conv weights in one launch: blockIdx.y = conv index.
+struct PackDesc {
+  const float* w;   // [K][R][S][C] fp32
+  bf16_t* fwd;      // [K][Kg] or null
+  bf16_t* dgrad;    // [C][R*S*K] or null
+  int K, RS, C, Cp, Kg, pad_;
+};
+
+__global__ __launch_bounds__(256) void pack_batched_kernel(const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const long long nf = d.fwd ? (long long)d.K * d.Kg : 0;
+  const long long nd = d.dgrad ? (long long)d.K * d.RS * d.C : 0;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < nf + nd; t += (long long)gridDim.x * blockDim.x) {
+    if (t < nf) {
+      const int k = (int)(t / d.Kg), col = (int)(t % d.Kg);
+      const int rs = col / d.Cp, c = col % d.Cp;
+      float val = 0.f;
+      if (rs < d.RS && c < d.C) val = d.w[((size_t)k * d.RS + rs) * d.C + c];
+      d.fwd[t] = f2bf(val);
+    } else {
+      const long long u = t - nf;
+      const int k = (int)(u % d.K);
+      const long long r2 = u / d.K;
+      const int rs = (int)(r2 % d.RS), c = (int)(r2 / d.RS);
+      d.dgrad[u] = f2bf(d.w[((size_t)k * d.RS + rs) * d.C + c]);
+    }
+  }
+}
+
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W,
                                     int Cp) {
   const long long total = (long long)N * H * W;
@@ -154,6 +183,20 @@ extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, 
     hipLaunchKernelGGL(pack_dgrad_kernel, dim3(grid_for((long long)K * R * S * C)), dim3(256), 0, st, w,
                        (bf16_t*)out_dgrad, K, R * S, C);
   return check_launch("pack_conv_weight");
+}
+
+// descs: device array of n records {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad}
+// (48 bytes each, layout of PackDesc); one launch packs every conv weight of the model.
+extern "C" size_t avt_pack_desc_bytes(void) { return sizeof(PackDesc); }
+
+extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream) {
+  AVT_REQUIRE(descs && n > 0, "pack_conv_weights_batched: bad arguments");
+  long long bx = (max_elems + 255) / 256;
+  if (bx > 512) bx = 512;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(pack_batched_kernel, dim3((unsigned)bx, n), dim3(256), 0, (hipStream_t)stream,
+                     (const PackDesc*)descs);
+  return check_launch("pack_conv_weights_batched");
 }
 
 extern "C" int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream) {

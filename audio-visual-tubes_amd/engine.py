@@ -160,6 +160,9 @@ class _EngineStore(Store):
     def packed(self, spec):
         return self.e.packs[spec.name]
 
+    def stat_acc(self, bn, kind):
+        return self.e.stat_views[(bn.prefix, kind)]
+
 
 class AVEngine:
     """Two trunks + the hard-way head on one device."""
@@ -171,21 +174,51 @@ class AVEngine:
         self.epsilon, self.epsilon2, self.tau, self.tri_map, self.neg = epsilon, epsilon2, tau, tri_map, neg
         self.store = _EngineStore(self)
         self.packs: Dict[str, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
+        self._pack_table = None
+        self._pack_max = 0
+        self.stat_views: Dict = {}
+        self._stat_arena = None
+        self._alloc(flat.flat.device)
+
+    def _alloc(self, dev):
+        """Persistent device buffers: packed bf16 weights, the batched-pack descriptor table and the
+        fp64 BN statistic accumulators (zero between uses)."""
+        import struct
+
+        descs = []
+        maxel = 0
+        for tr in (self.img, self.aud):
+            for spec in tr.convs():
+                wf = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+                wt = None if spec.is_stem else torch.empty(spec.cin, spec.k * spec.k * spec.cout, device=dev,
+                                                           dtype=torch.bfloat16)
+                self.packs[spec.name] = (wf, wt)
+                w = self.flat.raw(spec.name)
+                rs = spec.k * spec.k
+                descs.append(struct.pack("<QQQiiiiii", w.data_ptr(), wf.data_ptr(), 0 if wt is None else wt.data_ptr(),
+                                         spec.cout, rs, spec.cin, spec.cp, spec.kg, 0))
+                maxel = max(maxel, spec.cout * spec.kg + (0 if wt is None else wt.numel()))
+        assert len(descs[0]) == int(query("avt_pack_desc_bytes"))
+        blob = b"".join(descs)
+        self._pack_table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        self._pack_n, self._pack_max = len(descs), maxel
+        # BN accumulators: per BN 'fwd' [slots][C][3] f64 and 'bwd' [slots][C][2] f64 + k1/k2 (2C f32)
+        slots = int(query("avt_bn_slots"))
+        offs, total = {}, 0
+        for tr in (self.img, self.aud):
+            for bn in tr.bns():
+                n_f = slots * bn.c * 3
+                n_b = slots * bn.c * 2 + bn.c  # + 2C floats == C doubles
+                offs[(bn.prefix, "fwd")] = (total, n_f)
+                offs[(bn.prefix, "bwd")] = (total + n_f, n_b)
+                total += n_f + n_b
+        self._stat_arena = torch.zeros(total, device=dev, dtype=torch.float64)
+        self.stat_views = {k: self._stat_arena[o:o + n] for k, (o, n) in offs.items()}
 
     # ----------------------------------------------------------------------------- weights
     def pack_weights(self):
-        dev = self.flat.flat.device
-        for tr in (self.img, self.aud):
-            for spec in tr.convs():
-                w = self.flat.raw(spec.name)
-                if spec.name not in self.packs or self.packs[spec.name][0].device != dev:
-                    wf = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
-                    wt = None if spec.is_stem else torch.empty(spec.cin, spec.k * spec.k * spec.cout, device=dev,
-                                                               dtype=torch.bfloat16)
-                    self.packs[spec.name] = (wf, wt)
-                wf, wt = self.packs[spec.name]
-                call("avt_pack_conv_weight", P(w), spec.cout, spec.k, spec.k, spec.cin, spec.cp, spec.kg, P(wf), P(wt),
-                     stream_ptr())
+        """fp32 master weights -> bf16 fwd/dgrad operands of every conv, one launch."""
+        call("avt_pack_conv_weights_batched", P(self._pack_table), self._pack_n, self._pack_max, stream_ptr())
 
     # ----------------------------------------------------------------------------- forward
     @staticmethod
@@ -209,6 +242,7 @@ class AVEngine:
         self.pack_weights()
         if training:
             self.flat.nbt.add_(1)
+            self._stat_arena.zero_()  # accumulators are re-zeroed by their finalize; this is belt and braces
         xi = self._to_nhwc(image, 4)
         xa = self._to_nhwc(audio, 1)
         v, tape_i = self.img.forward(xi, self.store, training)

@@ -111,15 +111,18 @@ class Store:
     def buffer(self, name: str) -> torch.Tensor: ...
     def grad(self, name: str) -> Optional[torch.Tensor]: ...
     def packed(self, spec: ConvSpec): ...
+    def stat_acc(self, bn: "BNSpec", kind: str) -> torch.Tensor:
+        """Zeroed fp64 accumulator for a BN ('fwd': avt_bn_acc_doubles(C); 'bwd': bn_bwd workspace)."""
+        ...
 
 
-def _bn_finalize(c_out, partial, tiles, rows, bn: BNSpec, store: Store, training: bool, momentum=0.1, eps=1e-5):
+def _bn_finalize(c_out, acc, rows, bn: BNSpec, store: Store, training: bool, momentum=0.1, eps=1e-5):
     C = bn.c
     stats = torch.empty(4, C, device=c_out.device, dtype=torch.float32)  # scale, shift, mean, invstd
     gamma = store.param(bn.prefix + ".weight")
     beta = store.param(bn.prefix + ".bias")
     if training:
-        call("avt_bn_finalize", P(partial), tiles, rows, 128, C, P(gamma), P(beta),
+        call("avt_bn_finalize", P(acc), rows, C, P(gamma), P(beta),
              P(store.buffer(bn.prefix + ".running_mean")), P(store.buffer(bn.prefix + ".running_var")),
              ctypes.c_float(momentum), ctypes.c_float(eps), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]),
              stream_ptr())
@@ -181,14 +184,13 @@ class Trunk:
     def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool):
         Pq, Qq = conv_out(H, spec.k, spec.stride, spec.pad), conv_out(W, spec.k, spec.stride, spec.pad)
         y = torch.empty(N, Pq, Qq, spec.cout, device=x.device, dtype=torch.bfloat16)
-        tiles = query("avt_conv2d_fwd_stat_tiles", N, Pq, Qq)
-        partial = torch.empty(tiles, spec.cout, 2, device=x.device, dtype=torch.float32) if training else None
+        acc = store.stat_acc(bn, "fwd") if training else None
         wf, _ = store.packed(spec)
         ev = ConvProfiler.begin()
-        call("avt_conv2d_fwd", P(x), P(wf), P(y), P(partial), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
+        call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
              spec.stride, spec.pad, spec.kg, stream_ptr())
         ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin)
-        stats = _bn_finalize(y, partial, tiles, N * Pq * Qq, bn, store, training)
+        stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training)
         return y, stats, Pq, Qq
 
     def forward(self, x: torch.Tensor, store: Store, training: bool):
@@ -231,7 +233,7 @@ class Trunk:
     def _bn_bwd(self, g, y, xc, stats, bn: BNSpec, store: Store, gmask_out=None):
         rows = xc.numel() // bn.c
         gc = torch.empty_like(xc)
-        ws = torch.empty(int(query("avt_bn_bwd_workspace", rows, bn.c)), device=xc.device, dtype=torch.uint8)
+        ws = store.stat_acc(bn, "bwd")
         call("avt_bn_bwd", P(g), P(y), P(xc), P(stats[2]), P(stats[3]), P(store.param(bn.prefix + ".weight")),
              P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc), P(gmask_out), P(ws),
              rows, bn.c, stream_ptr())

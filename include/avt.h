@@ -38,11 +38,13 @@ const char* avt_last_error(void);
 int avt_abi_version(void);
 
 /* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
-/* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_partial != NULL also writes per-128-row
- * tile partials (sum, M2) of the fp32 result: float2[avt_conv2d_fwd_stat_tiles(N,P,Q)][K].
+/* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
+ * statistics are accumulated into bn_acc (fp64 [avt_bn_slots()][K][3], zero on entry, consumed and
+ * re-zeroed by avt_bn_finalize).
  * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
-int avt_conv2d_fwd_stat_tiles(int N, int P, int Q);
-int avt_conv2d_fwd(const void* x, const void* wpack, void* y, void* bn_partial, int N, int H, int W, int Cp, int K,
+int avt_bn_slots(void);
+size_t avt_bn_acc_doubles(int C);
+int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);
 /* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
 int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
@@ -52,13 +54,15 @@ int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int
                      int S, int stride, int pad, void* stream);
 
 /* ---- batch norm (train mode) ---- */
-int avt_bn_finalize(const void* partial, int ntiles, int rows, int tile_rows, int C, const float* gamma,
-                    const float* beta, float* running_mean, float* running_var, float momentum, float eps,
-                    float* scale, float* shift, float* save_mean, float* save_invstd, void* stream);
+/* merge bn_acc (see avt_conv2d_fwd) over `rows` rows -> scale, shift, mean, invstd (fp32 [C]);
+ * running stats updated if non-NULL (momentum, unbiased var); bn_acc re-zeroed */
+int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, float momentum, float eps, float* scale, float* shift, float* save_mean,
+                    float* save_invstd, void* stream);
 /* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
 int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                  const float* rshift, void* out, long long rows, int C, int relu, void* stream);
-int avt_bn_bwd_parts(long long rows, int C);
+/* bytes of bn_bwd workspace: its first avt_bn_slots()*C*2 doubles must be zero on entry (left zero) */
 size_t avt_bn_bwd_workspace(long long rows, int C);
 /* g' = g*[y>0] (y may be NULL: no mask); dgamma += sum g'*xhat; dbeta += sum g';
  * gc = gamma*invstd*(g' - mean(g') - xhat*mean(g'*xhat)); gmask_out (optional) = g' */
@@ -88,6 +92,10 @@ int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, void* stream);
 int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
                          void* stream);
+/* one launch for many convs: descs = device array of n records
+ * {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad;} (avt_pack_desc_bytes() each) */
+size_t avt_pack_desc_bytes(void);
+int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream);
 int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream);
 int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream);
 

@@ -82,20 +82,30 @@ def test_conv_fwd_and_bn_partials(case):
     wf, _ = pack(w.to(DEV), C, kg, with_t=False)
     xd = x.to(DEV)
     y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
-    tiles = query("avt_conv2d_fwd_stat_tiles", N, Pq, Qq)
-    part = torch.empty(tiles, K, 2, device=DEV)
-    call("avt_conv2d_fwd", P(xd), P(wf), P(y), P(part), N, H, W, C, K, R, R, st, pad, kg, S())
+    acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+    call("avt_conv2d_fwd", P(xd), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, kg, S())
     torch.cuda.synchronize()
     ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.to(torch.bfloat16).double().permute(0, 3, 1, 2), stride=st,
                    padding=pad).permute(0, 2, 3, 1)
     assert rel_err(y, ref) < 8e-3
     rows = ref.reshape(-1, K)
-    for t in range(tiles):
-        blk = rows[t * 128:(t + 1) * 128]
-        s = blk.sum(0)
-        m2 = ((blk - blk.mean(0)) ** 2).sum(0)
-        np.testing.assert_allclose(part[t, :, 0].double().cpu().numpy(), s.numpy(), rtol=1e-3, atol=1e-3 * blk.abs().max().item())
-        np.testing.assert_allclose(part[t, :, 1].double().cpu().numpy(), m2.numpy(), rtol=2e-3, atol=1e-3)
+    a = acc.view(-1, K, 3).sum(0).cpu()
+    n = rows.shape[0]
+    s_ref = rows.sum(0)
+    m2_ref = ((rows - rows.mean(0)) ** 2).sum(0)
+    np.testing.assert_allclose(a[:, 0].numpy(), s_ref.numpy(), rtol=1e-4, atol=1e-4 * rows.abs().max().item() * n ** 0.5)
+    m2 = a[:, 1] + a[:, 2] - a[:, 0] ** 2 / n
+    np.testing.assert_allclose(m2.numpy(), m2_ref.numpy(), rtol=1e-4)
+    # finalize consumes and re-zeroes the accumulator
+    gamma = torch.ones(K, device=DEV)
+    beta = torch.zeros(K, device=DEV)
+    stats = torch.empty(4, K, device=DEV)
+    call("avt_bn_finalize", P(acc), n, K, P(gamma), P(beta), None, None, ctypes.c_float(0.1), ctypes.c_float(1e-5),
+         P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
+    torch.cuda.synchronize()
+    assert acc.abs().max().item() == 0.0
+    np.testing.assert_allclose(stats[2].cpu().double().numpy(), rows.mean(0).numpy(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(stats[3].cpu().double().numpy(), (m2_ref / n + 1e-5).rsqrt().numpy(), rtol=1e-4)
 
 
 @pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
@@ -176,13 +186,19 @@ def test_wgrad_large_splitk():
 
 
 # ------------------------------------------------------------------------------------------ BN
-def _tile_partials(c):
+def _tile_acc(c):
+    """The accumulator a conv epilogue would leave: per 128-row tile t, (sum_t, M2_t, sum_t^2/n_t)
+    added into slot t % 16 (fp64)."""
     rows = c.double().reshape(-1, c.shape[-1])
-    parts = []
-    for t in range(0, rows.shape[0], 128):
+    C = rows.shape[1]
+    acc = torch.zeros(16, C, 3, dtype=torch.float64)
+    for i, t in enumerate(range(0, rows.shape[0], 128)):
         blk = rows[t:t + 128]
-        parts.append(torch.stack([blk.sum(0), ((blk - blk.mean(0)) ** 2).sum(0)], -1))
-    return torch.stack(parts).float()
+        s = blk.sum(0)
+        acc[i % 16, :, 0] += s
+        acc[i % 16, :, 1] += ((blk - blk.mean(0)) ** 2).sum(0)
+        acc[i % 16, :, 2] += s * s / blk.shape[0]
+    return acc.reshape(-1)
 
 
 @pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128)])
@@ -194,11 +210,11 @@ def test_bn_forward_train(shape):
     gamma = 1 + 0.02 * torch.randn(C, generator=g)
     beta = 0.1 * torch.randn(C, generator=g)
     rm, rv = torch.zeros(C), torch.ones(C)
-    part = _tile_partials(c).to(DEV)
+    acc = _tile_acc(c).to(DEV)
     stats = torch.empty(4, C, device=DEV)
     rmd, rvd = rm.to(DEV), rv.to(DEV)
     rows = N * H * W
-    call("avt_bn_finalize", P(part), part.shape[0], rows, 128, C, P(gamma.to(DEV)), P(beta.to(DEV)), P(rmd), P(rvd),
+    call("avt_bn_finalize", P(acc), rows, C, P(gamma.to(DEV)), P(beta.to(DEV)), P(rmd), P(rvd),
          ctypes.c_float(0.1), ctypes.c_float(1e-5), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
     out = torch.empty_like(c, device=DEV)
     call("avt_bn_apply", P(c.to(DEV)), P(stats[0]), P(stats[1]), P(res.to(DEV)), None, None, P(out), rows, C, 1, S())
@@ -232,7 +248,7 @@ def test_bn_backward(shape, masked):
     inv = (var + 1e-5).rsqrt()
     yd = y.detach().permute(0, 2, 3, 1).to(torch.bfloat16).to(DEV).contiguous()
     rows = N * H * W
-    ws = torch.empty(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
+    ws = torch.zeros(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
     dgamma = torch.zeros(C, device=DEV)
     dbeta = torch.zeros(C, device=DEV)
     gc = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
