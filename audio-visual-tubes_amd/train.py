@@ -2,10 +2,12 @@
 
 Equivalent to one iteration of train_hardway_1frame.py:121-135 with the model wrapped for data
 parallelism.  The reference uses ``nn.DataParallel`` (train_hardway_1frame.py:93): each replica
-contrasts only its own B/G samples (model.py:114-115) and gradients are reduced to GPU 0.  Here
-each process owns one GPU and its local batch (same local-negative semantics), gradients are
-averaged with ONE all-reduce of the flat fp32 gradient buffer over RCCL (backend "nccl"), and BN
-running statistics follow rank 0 (DDP ``broadcast_buffers``, matching DP's replica-0 buffers).
+contrasts only its own B/G samples (model.py:114-115), its BN uses its local batch statistics, and
+the loss is the mean over the gathered logits, so the gradient is the mean of the replicas' local
+mean-CE gradients.  Here each process owns one GPU and its local batch (same local-negative
+semantics); gradients are summed with ONE all-reduce of the flat fp32 gradient buffer over RCCL
+(backend "nccl"), the 1/world factor is folded into the Adam kernel, and BN running statistics
+follow rank 0 (DDP ``broadcast_buffers``, matching DP's replica-0 buffers).
 """
 from __future__ import annotations
 
@@ -18,6 +20,25 @@ from .engine import AVEngine
 from .optim import FlatAdam
 
 
+def world_size(pg: Optional[dist.ProcessGroup] = None) -> int:
+    return dist.get_world_size(pg) if dist.is_available() and dist.is_initialized() else 1
+
+
+def sync_gradients(grad: torch.Tensor, pg: Optional[dist.ProcessGroup] = None) -> float:
+    """Sum the flat gradient over ranks in place (one collective); return the scale (1/world) that
+    turns the sum into the data-parallel mean."""
+    w = world_size(pg)
+    if w > 1:
+        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=pg)
+    return 1.0 / w
+
+
+def sync_buffers(bflat: torch.Tensor, pg: Optional[dist.ProcessGroup] = None):
+    """BN running statistics follow rank 0 (torch DDP broadcast_buffers semantics)."""
+    if world_size(pg) > 1:
+        dist.broadcast(bflat, 0, group=pg)
+
+
 class HardWayTrainStep:
     def __init__(self, model, lr: float = 1e-6, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  process_group: Optional[dist.ProcessGroup] = None):
@@ -27,22 +48,18 @@ class HardWayTrainStep:
         self.opt = FlatAdam(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.grad = torch.zeros(self.flat.n_train, device=self.flat.flat.device, dtype=torch.float32)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
+        self.world = world_size(process_group)
         if self.world > 1:
             # start from identical weights everywhere (DDP constructor semantics)
             dist.broadcast(self.flat.flat, 0, group=self.pg)
-            dist.broadcast(self.flat.bflat, 0, group=self.pg)
+            sync_buffers(self.flat.bflat, self.pg)
 
     def step(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
         """Returns the local mean CE loss (device scalar, no host sync)."""
-        if self.world > 1:
-            dist.broadcast(self.flat.bflat, 0, group=self.pg)  # BN running stats follow rank 0
+        sync_buffers(self.flat.bflat, self.pg)
         out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
         self.grad.zero_()
         self.engine.backward(tape, out["dlogits"], self.grad)
-        scale = 1.0
-        if self.world > 1:
-            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.pg)
-            scale = 1.0 / self.world
+        scale = sync_gradients(self.grad, self.pg)
         self.opt.step(self.grad, grad_scale=scale)
         return out["loss"]

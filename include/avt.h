@@ -43,6 +43,11 @@ int avt_abi_version(void);
  * re-zeroed by avt_bn_finalize).
  * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
 int avt_bn_slots(void);
+/* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
+ * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
+int avt_set_conv_variant(int variant);
+/* wgrad split-K policy: about target_blocks blocks in total, at least min_ktiles 32-pixel tiles each */
+int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);

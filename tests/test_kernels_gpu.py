@@ -108,6 +108,32 @@ def test_conv_fwd_and_bn_partials(case):
     np.testing.assert_allclose(stats[3].cpu().double().numpy(), (m2_ref / n + 1e-5).rsqrt().numpy(), rtol=1e-4)
 
 
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_variants_bitwise_equal(case):
+    """The LDS-DMA pipelined kernel and the register-staged one sum in the same order."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 31).relu().to(DEV)
+    g = torch.Generator().manual_seed(32)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, R * R * C)
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    dy = _rand_act(N, Pq, Qq, K, 33).to(DEV)
+    outs = []
+    try:
+        for variant in (0, 1):
+            call("avt_set_conv_variant", variant)
+            y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), None, N, H, W, C, K, R, R, st, pad, R * R * C, S())
+            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), P(x), N, H, W, C, K, R, R, st, pad, S())
+            outs.append((y, dx))
+    finally:
+        call("avt_set_conv_variant", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
 def test_stem_fwd_wgrad(cin, cp, H, W):
     N, K, R, st, pad = 2, 64, 7, 2, 3

@@ -1,0 +1,106 @@
+"""Per-shape microbenchmark of the libavt conv kernels (fwd / dgrad / wgrad) at the B=128 trunk
+shapes.  Prints TFLOP/s per (shape, kind[, variant]).  Usage: python tools/conv_bench.py [--batch 128]"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import avtubes  # noqa: E402,F401
+from avt_amd._lib import call  # noqa: E402
+
+# (name, H, W, C, K, R, stride, pad)
+SHAPES = [
+    ("V.l1 3x3", 56, 56, 64, 64, 3, 1, 1),
+    ("V.l2 3x3", 28, 28, 128, 128, 3, 1, 1),
+    ("V.l2.0 s2", 56, 56, 64, 128, 3, 2, 1),
+    ("V.l3 3x3", 14, 14, 256, 256, 3, 1, 1),
+    ("V.l4 3x3", 14, 14, 512, 512, 3, 1, 1),
+    ("V.l4.0 256", 14, 14, 256, 512, 3, 1, 1),
+    ("A.l1 3x3", 65, 75, 64, 64, 3, 1, 1),
+    ("A.l2 3x3", 33, 38, 128, 128, 3, 1, 1),
+    ("A.l3 3x3", 17, 19, 256, 256, 3, 1, 1),
+    ("A.l4 3x3", 17, 19, 512, 512, 3, 1, 1),
+    ("A.ds 1x1s2", 33, 38, 128, 256, 1, 2, 0),
+]
+
+
+def P(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--only", default="")
+    ap.add_argument("--wgrad-policy", default="512,16;1024,8;2048,4;256,32")
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    N = args.batch
+    kinds = args.kinds.split(",")
+    tot = {}
+    for name, H, W, C, K, R, st, pad in SHAPES:
+        if args.only and args.only not in name:
+            continue
+        Pq, Qq = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+        x = torch.randn(N, H, W, C, device=dev).relu().to(torch.bfloat16)
+        dy = torch.randn(N, Pq, Qq, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(K, R, R, C, device=dev) * 0.05
+        kg = R * R * C
+        wf = torch.empty(K, kg, device=dev, dtype=torch.bfloat16)
+        wt = torch.empty(C, R * R * K, device=dev, dtype=torch.bfloat16)
+        call("avt_pack_conv_weight", P(w), K, R, R, C, C, kg, P(wf), P(wt), S())
+        y = torch.empty(N, Pq, Qq, K, device=dev, dtype=torch.bfloat16)
+        dx = torch.empty(N, H, W, C, device=dev, dtype=torch.bfloat16)
+        dw = torch.zeros(K, R, R, C, device=dev)
+        acc = torch.zeros(16 * K * 3, device=dev, dtype=torch.float64)
+        flops = 2.0 * N * Pq * Qq * K * C * R * R
+        line = f"{name:12s} M={N * Pq * Qq:7d} N={K:4d} K={kg:5d}"
+        for v in [int(s) for s in args.variants.split(",")]:
+            call("avt_set_conv_variant", v)
+            if "fwd" in kinds:
+                ms = timeit(lambda: call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad,
+                                         kg, S()))
+                line += f" | v{v} fwd {flops / ms / 1e9:6.0f}"
+                tot[("fwd", v)] = tot.get(("fwd", v), 0) + ms
+            if "dgrad" in kinds:
+                ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad,
+                                         S()))
+                line += f" dgrad {flops / ms / 1e9:6.0f}"
+                tot[("dgrad", v)] = tot.get(("dgrad", v), 0) + ms
+            if "wgrad" in kinds and v == 1:
+                for pol in args.wgrad_policy.split(";"):
+                    tb, mk = (int(s) for s in pol.split(","))
+                    call("avt_set_wgrad_policy", tb, mk)
+                    ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st, pad,
+                                             S()))
+                    line += f" wgrad[{tb},{mk}] {flops / ms / 1e9:6.0f}"
+                    tot[("wgrad" + pol, v)] = tot.get(("wgrad" + pol, v), 0) + ms
+                call("avt_set_wgrad_policy", 512, 16)
+        print(line + "  TFLOP/s", flush=True)
+    call("avt_set_conv_variant", 1)
+    print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
+
+
+if __name__ == "__main__":
+    main()
