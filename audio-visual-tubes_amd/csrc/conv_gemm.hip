@@ -454,240 +454,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// NT kernel, LDS-DMA pipeline (fwd / dgrad, C % 32 == 0): every operand chunk goes global -> LDS
-// with global_load_lds_dwordx4 (per-lane gather address, lane-linear LDS image, XOR swizzle on the
-// SOURCE chunk), NST-deep ring with NST-1 tiles in flight, counted vmcnt + raw s_barrier (one per
-// k-tile), XCD-aware tile order.  Out-of-image taps load from a zero page.
-// ------------------------------------------------------------------------------------------------
-__device__ __attribute__((aligned(64))) bf16_t g_zero_page[64];
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
-
-// 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32.
-template <int MODE, int WM, int WN, int TM, int TN, int NST>
-__global__ __launch_bounds__(256) void conv_nt_glds_kernel(GemmNTParams p) {
-  static_assert(WM * WN == 4, "4 waves");
-  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int AR = BM / 64, BR = BN / 64;  // glds instructions per wave per tile (16 rows each)
-  constexpr int LPT = AR + BR;
-  constexpr int STAGE = (BM + BN) * 64;
-  constexpr int CT_LD = BN + 8;
-  constexpr int EPI_BYTES = BM * CT_LD * 2;
-  constexpr int SMEM = (NST * STAGE > EPI_BYTES ? NST * STAGE : EPI_BYTES);
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * WM * BN * 4];
-  float* red = reinterpret_cast<float*>(smem + SMEM);  // [2][WM][BN]
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const int nnt = p.Ng / BN;
-  const int nwg = gridDim.x;
-  const int bid = xcd_remap(blockIdx.x, nwg);
-  const int mt = bid / nnt, nt = bid - mt * nnt;
-  const int m0 = mt * BM, n0 = nt * BN;
-
-  // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*16 + lane/4 ----
-  const int lrow = lane >> 2, pchunk = lane & 3;
-  int a_pix[AR], a_y[AR], a_x[AR], a_lc[AR];
-  bool a_ok[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int row = (wid * AR + i) * 16 + lrow;
-    a_lc[i] = pchunk ^ ((row >> 2) & 3);
-    const int m = m0 + row;
-    a_ok[i] = m < p.M;
-    const int mm = a_ok[i] ? m : 0;
-    const int hw = p.OH * p.OW;
-    const int n = mm / hw, rem = mm - n * hw;
-    const int oh = rem / p.OW, ow = rem - oh * p.OW;
-    a_pix[i] = n * p.IH * p.IW;
-    if (MODE == MODE_FWD) {
-      a_y[i] = oh * p.stride - p.pad;
-      a_x[i] = ow * p.stride - p.pad;
-    } else {
-      a_y[i] = oh + p.pad;
-      a_x[i] = ow + p.pad;
-    }
-  }
-  const bf16_t* bsrc[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int row = (wid * BR + i) * 16 + lrow;
-    bsrc[i] = p.wmat + (size_t)(n0 + row) * p.Kg + ((pchunk ^ ((row >> 2) & 3)) * 8);
-  }
-  typedef __attribute__((address_space(3))) void lds_void;
-  const int nkt = p.Kg / 32;
-
-  auto issue = [&](int kt, int stage) {
-    const int k0 = kt * 32;
-    const int rs = k0 / p.IC, c0 = k0 - rs * p.IC;
-    const int r = rs / p.S, s = rs - r * p.S;
-    char* As = smem + stage * STAGE;
-    char* Bs = As + BM * 64;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      int y, x;
-      bool ok = a_ok[i];
-      if (MODE == MODE_FWD) {
-        y = a_y[i] + r;
-        x = a_x[i] + s;
-      } else {
-        int yn = a_y[i] - r, xn = a_x[i] - s;
-        if (p.stride == 2) {
-          ok = ok && ((yn & 1) == 0) && ((xn & 1) == 0);
-          yn >>= 1;
-          xn >>= 1;
-        }
-        y = yn;
-        x = xn;
-      }
-      ok = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
-      const bf16_t* src = ok ? p.act + (size_t)(a_pix[i] + y * p.IW + x) * p.IC + c0 + a_lc[i] * 8 : g_zero_page;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(As + (wid * AR + i) * 1024), 16, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + k0), (lds_void*)(Bs + (wid * BR + i) * 1024), 16, 0, 0);
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
-    if (t < nkt) issue(t, t);
-
-  const int frow = lane & 31, fhalf = lane >> 5;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int rem = nkt - 1 - kt;  // tiles issued after kt (capped at NST-2)
-    if (rem >= NST - 2)
-      wait_vmcnt<(NST - 2) * LPT>();
-    else if (rem == 1)
-      wait_vmcnt<LPT>();
-    else
-      wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + NST - 1 < nkt) issue(kt + NST - 1, (kt + NST - 1) % NST);
-    const char* As = smem + (kt % NST) * STAGE;
-    const char* Bs = As + BM * 64;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / WM) + i * 32 + frow;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz64(row, ks * 2 + fhalf));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / WN) + j * 32 + frow;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(row, ks * 2 + fhalf));
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();
-
-  // ---- epilogue: BN partial statistics, then the bf16 tile through LDS ----
-  const int rows_valid = min(BM, p.M - m0);
-  if (MODE == MODE_FWD && p.stats != nullptr) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-          if (r < rows_valid) s += acc[i][j][v];
-        }
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 32) red[wm * BN + wn * (BN / WN) + j * 32 + lane] = s;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int c = wn * (BN / WN) + j * 32 + frow;
-      float tot = 0.f;
-#pragma unroll
-      for (int k = 0; k < WM; ++k) tot += red[k * BN + c];
-      const float mean = tot / (float)rows_valid;
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-          const float d = acc[i][j][v] - mean;
-          if (r < rows_valid) q += d * d;
-        }
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 32) red[WM * BN + wm * BN + c] = q;
-    }
-    __syncthreads();
-    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
-    for (int c = tid; c < BN; c += 256) {
-      double s = 0.0, m2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < WM; ++k) {
-        s += (double)red[k * BN + c];
-        m2 += (double)red[WM * BN + k * BN + c];
-      }
-      double* a = acc_slot + (size_t)(n0 + c) * 3;
-      atomicAdd(a + 0, s);
-      atomicAdd(a + 1, m2);
-      atomicAdd(a + 2, s * s / (double)rows_valid);
-    }
-  }
-  bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-        const int c = wn * (BN / WN) + j * 32 + frow;
-        Ct[r * CT_LD + c] = f2bf(acc[i][j][v]);
-      }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int idx = tid; idx < BM * CPR; idx += 256) {
-    const int r = idx / CPR, cc = idx - r * CPR;
-    if (r >= rows_valid) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
-    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
-    if (p.add != nullptr) {
-      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
-      unsigned* vv = reinterpret_cast<unsigned*>(&v);  // (glds variant)
-      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
-        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
-        vv[e] = pack2(lo, hi);
-      }
-    }
-    *reinterpret_cast<u32x4*>(p.out + off) = v;
-  }
-}
+#include "conv_nt_pipe.h"
 
 static int g_wgrad_blocks = 512;  // split-K policy of the wgrad kernel (tunable for A/B runs)
 static int g_wgrad_min_kt = 16;
@@ -725,7 +492,15 @@ template <int MODE, int WM, int WN, int TM, int TN>
 static void launch_glds(const GemmNTParams& p, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
-  hipLaunchKernelGGL((conv_nt_glds_kernel<MODE, WM, WN, TM, TN, 4>), dim3(grid), dim3(256), 0, st, p);
+  const unsigned act_bytes = (unsigned)((size_t)(MODE == MODE_FWD ? p.M / (p.OH * p.OW) : p.M / (p.OH * p.OW)) *
+                                        p.IH * p.IW * p.IC * 2);
+  const unsigned w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
+  if (MODE == MODE_DGRAD && p.stride == 2)
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, 2, WM, WN, TM, TN, 4>), dim3(grid), dim3(256), 0, st, p, act_bytes,
+                       w_bytes);
+  else
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, 1, WM, WN, TM, TN, 4>), dim3(grid), dim3(256), 0, st, p, act_bytes,
+                       w_bytes);
 }
 
 template <int MODE, int CVEC, int BM, int BN>

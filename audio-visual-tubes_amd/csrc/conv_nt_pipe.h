@@ -1,0 +1,274 @@
+// NT implicit-GEMM convolution, LDS-DMA pipeline (fwd / dgrad, C % 32 == 0).  Included by
+// conv_gemm.hip inside namespace avt (needs GemmNTParams, swz64, MODE_*).
+//
+// Every operand chunk goes global -> LDS with `buffer_load_dwordx4 ... lds` (per-lane byte offset,
+// lane-linear LDS image, XOR swizzle applied to the SOURCE chunk).  Out-of-image / wrong-parity
+// taps get an out-of-range offset, so the buffer unit writes zeros (no branches, no zero page).
+// Per lane and row the gather offset of tap (0,0) and a bitmask of valid taps are precomputed; a
+// k-tile costs 3 VALU per gathered row and a handful of SALU.  NST-stage ring, NST-1 tiles in
+// flight, one counted vmcnt + raw s_barrier per k-tile (tiles past the end are issued as all-OOB
+// dummies so the count is constant), XCD-aware tile order.
+#pragma once
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+constexpr unsigned kOOB = 0x80000000u;  // beyond any activation buffer: the load returns zeros
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+// 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32.
+template <int MODE, int STRIDE, int WM, int WN, int TM, int TN, int NST>
+__global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsigned act_bytes, unsigned w_bytes) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int AR = BM / 64, BR = BN / 64;  // buffer-lds instructions per wave per tile (16 rows each)
+  constexpr int LPT = AR + BR;
+  constexpr int STAGE = (BM + BN) * 64;
+  constexpr int CT_LD = BN + 8;
+  constexpr int EPI_BYTES = BM * CT_LD * 2;
+  constexpr int SMEM = (NST * STAGE > EPI_BYTES ? NST * STAGE : EPI_BYTES);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * WM * BN * 4];
+  float* red = reinterpret_cast<float*>(smem + SMEM);  // [2][WM][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int nnt = p.Ng / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)act_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.wmat, (short)0, (int)w_bytes, 0x00020000);
+
+  // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*16 + lane/4 ----
+  const int lrow = lane >> 2, pchunk = lane & 3;
+  unsigned a_off0[AR], a_mask[AR];
+  int a_py[AR], a_px[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int row = (wid * AR + i) * 16 + lrow;
+    const int lc = pchunk ^ ((row >> 2) & 3);
+    const int m = m0 + row;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    const int hw = p.OH * p.OW;
+    const int n = mm / hw, rem = mm - n * hw;
+    const int oh = rem / p.OW, ow = rem - oh * p.OW;
+    int yb, xb;  // source coordinate of tap (0,0)
+    if (MODE == MODE_FWD) {
+      yb = oh * p.stride - p.pad;
+      xb = ow * p.stride - p.pad;
+    } else if (STRIDE == 1) {
+      yb = oh + p.pad;  // tap (r,s) reads y = yb - r
+      xb = ow + p.pad;
+    } else {
+      a_py[i] = (oh + p.pad) & 1;
+      a_px[i] = (ow + p.pad) & 1;
+      yb = (oh + p.pad) >> 1;  // tap (r,s) valid iff r == py (mod 2); reads y = yb - (r - py)/2
+      xb = (ow + p.pad) >> 1;
+    }
+    unsigned mask = 0;
+    for (int r = 0; r < p.R; ++r)
+      for (int s = 0; s < p.S; ++s) {
+        int y, x;
+        bool v = ok;
+        if (MODE == MODE_FWD) {
+          y = yb + r;
+          x = xb + s;
+        } else if (STRIDE == 1) {
+          y = yb - r;
+          x = xb - s;
+        } else {
+          v = v && ((r & 1) == a_py[i]) && ((s & 1) == a_px[i]);
+          y = yb - ((r - a_py[i]) >> 1);
+          x = xb - ((s - a_px[i]) >> 1);
+        }
+        v = v && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
+        mask |= (v ? 1u : 0u) << (r * p.S + s);
+      }
+    a_mask[i] = mask;
+    a_off0[i] = (unsigned)(((long long)n * p.IH * p.IW + (long long)yb * p.IW + xb) * p.IC + lc * 8) * 2u;
+  }
+  unsigned b_off[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int row = (wid * BR + i) * 16 + lrow;
+    b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + ((pchunk ^ ((row >> 2) & 3)) * 8)) * 2);
+  }
+  const int nkt = p.Kg / 32;
+
+  // incremental tap state of the next tile to issue (wave-uniform)
+  int it_r = 0, it_s = 0, it_c = 0, it_k = 0;
+  auto issue = [&](int stage) {
+    char* As = smem + stage * STAGE;
+    char* Bs = As + BM * 64;
+    const bool live = it_k < nkt;
+    const int t = it_r * p.S + it_s;
+    int tapoff;  // byte offset of tap (r,s) channel block c relative to tap (0,0)
+    if (MODE == MODE_FWD)
+      tapoff = ((it_r * p.IW + it_s) * p.IC + it_c) * 2;
+    else
+      tapoff = (it_c - (it_r * p.IW + it_s) * p.IC) * 2;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      unsigned voff;
+      if (MODE == MODE_DGRAD && STRIDE == 2) {
+        const int dy = (it_r - a_py[i]) >> 1, dx = (it_s - a_px[i]) >> 1;
+        voff = a_off0[i] + (unsigned)((it_c - (dy * p.IW + dx) * p.IC) * 2);
+      } else {
+        voff = a_off0[i] + (unsigned)tapoff;
+      }
+      voff = (live && ((a_mask[i] >> t) & 1u)) ? voff : kOOB;
+      buf_lds16(rsa, As + (wid * AR + i) * 1024, voff);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + (unsigned)(it_k * 64) : kOOB);
+    // advance
+    ++it_k;
+    it_c += 32;
+    if (it_c == p.IC) {
+      it_c = 0;
+      if (++it_s == p.S) {
+        it_s = 0;
+        ++it_r;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t) issue(t);
+
+  const int frow = lane & 31, fhalf = lane >> 5;
+  for (int kt = 0; kt < nkt; ++kt) {
+    wait_vmcnt<(NST - 2) * LPT>();  // tile kt has landed (NST-2 younger tiles may be in flight)
+    __builtin_amdgcn_s_barrier();
+    issue((kt + NST - 1) % NST);  // the stage read in iteration kt-1; every wave has passed that
+    const char* As = smem + (kt % NST) * STAGE;
+    const char* Bs = As + BM * 64;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * (BM / WM) + i * 32 + frow;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + swz64(row, ks * 2 + fhalf));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / WN) + j * 32 + frow;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(row, ks * 2 + fhalf));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt<0>();  // drain the dummy tail loads before the ring is reused
+  __syncthreads();
+
+  // ---- epilogue: BN partial statistics, then the bf16 tile through LDS ----
+  const int rows_valid = min(BM, p.M - m0);
+  if (MODE == MODE_FWD && p.stats != nullptr) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          if (r < rows_valid) s += acc[i][j][v];
+        }
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 32) red[wm * BN + wn * (BN / WN) + j * 32 + lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = wn * (BN / WN) + j * 32 + frow;
+      float tot = 0.f;
+#pragma unroll
+      for (int k = 0; k < WM; ++k) tot += red[k * BN + c];
+      const float mean = tot / (float)rows_valid;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          const float d = acc[i][j][v] - mean;
+          if (r < rows_valid) q += d * d;
+        }
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 32) red[WM * BN + wm * BN + c] = q;
+    }
+    __syncthreads();
+    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
+    for (int c = tid; c < BN; c += 256) {
+      double s = 0.0, m2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < WM; ++k) {
+        s += (double)red[k * BN + c];
+        m2 += (double)red[WM * BN + k * BN + c];
+      }
+      double* a = acc_slot + (size_t)(n0 + c) * 3;
+      atomicAdd(a + 0, s);
+      atomicAdd(a + 1, m2);
+      atomicAdd(a + 2, s * s / (double)rows_valid);
+    }
+  }
+  bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        const int c = wn * (BN / WN) + j * 32 + frow;
+        Ct[r * CT_LD + c] = f2bf(acc[i][j][v]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int idx = tid; idx < BM * CPR; idx += 256) {
+    const int r = idx / CPR, cc = idx - r * CPR;
+    if (r >= rows_valid) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
+    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
+    if (p.add != nullptr) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+      unsigned* vv = reinterpret_cast<unsigned*>(&v);
+      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
+        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
+        vv[e] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(p.out + off) = v;
+  }
+}
