@@ -29,6 +29,7 @@ SIGNATURES = {
     "avt_bn_slots": (_I, []),
     "avt_set_conv_variant": (_I, [_I]),
     "avt_set_wgrad_policy": (_I, [_I, _I]),
+    "avt_set_nt64_config": (_I, [_I]),
     "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

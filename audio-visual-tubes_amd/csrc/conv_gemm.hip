@@ -455,9 +455,11 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 }
 
 #include "conv_nt_pipe.h"
+#include "conv_tn_pipe.h"
 
-static int g_wgrad_blocks = 512;  // split-K policy of the wgrad kernel (tunable for A/B runs)
-static int g_wgrad_min_kt = 16;
+static int g_nt64_config = 1;  // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
+static int g_wgrad_blocks = 1024;  // split-K policy of the wgrad kernel (tunable for A/B runs)
+static int g_wgrad_min_kt = 8;
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -476,6 +478,12 @@ extern "C" int avt_set_conv_variant(int v) {
   return AVT_OK;
 }
 
+extern "C" int avt_set_nt64_config(int cfg) {
+  AVT_REQUIRE(cfg >= 0 && cfg <= 3, "set_nt64_config: cfg in 0..3");
+  g_nt64_config = cfg;
+  return AVT_OK;
+}
+
 extern "C" int avt_set_wgrad_policy(int target_blocks, int min_ktiles) {
   AVT_REQUIRE(target_blocks >= 1 && min_ktiles >= 1, "set_wgrad_policy: bad arguments");
   avt::g_wgrad_blocks = target_blocks;
@@ -488,28 +496,74 @@ extern "C" int avt_set_wgrad_policy(int target_blocks, int min_ktiles) {
 // ------------------------------------------------------------------------------------------------
 static inline int conv_out(int in, int k, int st, int pad) { return (in + 2 * pad - k) / st + 1; }
 
-template <int MODE, int WM, int WN, int TM, int TN>
-static void launch_glds(const GemmNTParams& p, hipStream_t st) {
+template <int MODE, int WM, int WN, int TM, int TN, int NST>
+static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgs& ta, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
-  const unsigned act_bytes = (unsigned)((size_t)(MODE == MODE_FWD ? p.M / (p.OH * p.OW) : p.M / (p.OH * p.OW)) *
-                                        p.IH * p.IW * p.IC * 2);
-  const unsigned w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
-  if (MODE == MODE_DGRAD && p.stride == 2)
-    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, 2, WM, WN, TM, TN, 4>), dim3(grid), dim3(256), 0, st, p, act_bytes,
-                       w_bytes);
-  else
-    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, 1, WM, WN, TM, TN, 4>), dim3(grid), dim3(256), 0, st, p, act_bytes,
-                       w_bytes);
+  if (grid > 0)
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST>), dim3(grid), dim3(256), 0, st, p, ta);
+}
+
+// Builds the tap list(s) and launches: fwd / stride-1 dgrad in one launch; a stride-2 dgrad as
+// four parity-class launches, each walking only its class's taps.
+template <int MODE, int WM, int WN, int TM, int TN, int NST = 4>
+static void launch_glds(const GemmNTParams& p, hipStream_t st) {
+  NTPipeArgs ta{};
+  const int batch = p.M / (p.OH * p.OW);
+  ta.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * p.IC * 2);
+  ta.w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
+  if (MODE == MODE_FWD || p.stride == 1) {
+    ta.ntaps = p.R * p.S;
+    for (int r = 0; r < p.R; ++r)
+      for (int s = 0; s < p.S; ++s) {
+        const int t = r * p.S + s;
+        ta.tap_w[t] = t;
+        ta.tap_dy[t] = MODE == MODE_FWD ? r - p.pad : p.pad - r;
+        ta.tap_dx[t] = MODE == MODE_FWD ? s - p.pad : p.pad - s;
+      }
+    launch_pipe_one<MODE, WM, WN, TM, TN, NST>(p, ta, st);
+    return;
+  }
+  ta.cls = 1;
+  ta.OHf = p.OH;
+  ta.OWf = p.OW;
+  for (int ph = 0; ph < 2; ++ph)
+    for (int pw = 0; pw < 2; ++pw) {
+      NTPipeArgs tc = ta;
+      tc.ph = ph;
+      tc.pw = pw;
+      tc.ntaps = 0;
+      for (int r = 0; r < p.R; ++r)
+        for (int s = 0; s < p.S; ++s) {
+          if (((ph + p.pad - r) & 1) || ((pw + p.pad - s) & 1)) continue;
+          tc.tap_w[tc.ntaps] = r * p.S + s;
+          tc.tap_dy[tc.ntaps] = (ph + p.pad - r) / 2;
+          tc.tap_dx[tc.ntaps] = (pw + p.pad - s) / 2;
+          ++tc.ntaps;
+        }
+      GemmNTParams pc = p;
+      pc.OH = (p.OH - ph + 1) / 2;
+      pc.OW = (p.OW - pw + 1) / 2;
+      pc.M = batch * pc.OH * pc.OW;
+      // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) still runs with an
+      // empty K loop: its rows are written as 0 (+ add)
+      launch_pipe_one<MODE, WM, WN, TM, TN, NST>(pc, tc, st);
+    }
 }
 
 template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
   if (CVEC == 8 && conv_variant() == 1) {
-    if (p.Ng % 128 == 0)
+    if (p.Ng % 128 == 0) {
       launch_glds<MODE, 2, 2, 2, 2>(p, st);  // 128 x 128
-    else
-      launch_glds<MODE, 4, 1, 2, 2>(p, st);  // 256 x 64 (layer1: 64 channels)
+    } else {  // 64-wide N (layer1 / stem-fed convs)
+      switch (g_nt64_config) {
+        case 0: launch_glds<MODE, 4, 1, 2, 2, 4>(p, st); break;  // 256 x 64, 4 stages
+        case 2: launch_glds<MODE, 2, 2, 2, 1, 4>(p, st); break;  // 128 x 64, 4 stages
+        case 3: launch_glds<MODE, 4, 1, 2, 2, 2>(p, st); break;  // 256 x 64, 2 stages
+        default: launch_glds<MODE, 2, 2, 2, 1, 3>(p, st); break;  // 128 x 64, 3 stages
+      }
+    }
     return;
   }
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
@@ -591,6 +645,17 @@ static void launch_tn(GemmTNParams p, hipStream_t st) {
   if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;
   splits = (nkt + kps - 1) / kps;
   p.kt_per_split = kps;
+  if (CVEC == 8 && conv_variant() == 1) {
+    GemmTNPipeParams pp;
+    pp.p = p;
+    pp.div_pq = make_magic((unsigned)(p.P * p.Q));
+    pp.div_q = make_magic((unsigned)p.Q);
+    pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
+    pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
+    constexpr int TM = BM / 64, TN = BN / 64;
+    hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, TM, TN, 4>), dim3(tiles * splits), dim3(256), 0, st, pp);
+    return;
+  }
   hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(tiles, splits), dim3(256), 0, st, p);
 }
 

@@ -2,12 +2,15 @@
 // conv_gemm.hip inside namespace avt (needs GemmNTParams, swz64, MODE_*).
 //
 // Every operand chunk goes global -> LDS with `buffer_load_dwordx4 ... lds` (per-lane byte offset,
-// lane-linear LDS image, XOR swizzle applied to the SOURCE chunk).  Out-of-image / wrong-parity
-// taps get an out-of-range offset, so the buffer unit writes zeros (no branches, no zero page).
-// Per lane and row the gather offset of tap (0,0) and a bitmask of valid taps are precomputed; a
-// k-tile costs 3 VALU per gathered row and a handful of SALU.  NST-stage ring, NST-1 tiles in
-// flight, one counted vmcnt + raw s_barrier per k-tile (tiles past the end are issued as all-OOB
-// dummies so the count is constant), XCD-aware tile order.
+// lane-linear LDS image, XOR swizzle applied to the SOURCE chunk).  Out-of-image taps get an
+// out-of-range offset, so the buffer unit writes zeros (no branches, no zero page).  The K loop
+// walks an explicit tap list: all R*S taps, or — for the dgrad of a stride-2 conv — only the
+// taps of one output parity class (rows are the pixels (2h'+ph, 2w'+pw) of that class), which
+// removes the 3/4 of zero work a plain gather-dgrad would do.  Per lane and row the offset of the
+// class origin and a bitmask of in-image taps are precomputed; a k-tile costs ~3 VALU per
+// gathered row.  NST-stage ring, NST-1 tiles in flight, one counted vmcnt + raw s_barrier per
+// k-tile (tiles past the end are issued as all-OOB dummies so the count is constant), XCD-aware
+// tile order.
 #pragma once
 
 template <int N>
@@ -28,9 +31,19 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_w
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_wave_base, 16, voff, 0, 0, 0);
 }
 
+struct NTPipeArgs {
+  unsigned act_bytes, w_bytes;
+  int ntaps;              // taps in the K loop
+  int tap_w[9];           // weight tap index r*S+s of each listed tap
+  int tap_dy[9], tap_dx[9];  // source displacement of each tap relative to the row origin
+  int cls;                // 1: rows are one parity class of a stride-2 dgrad output
+  int ph, pw;             // that class
+  int OHf, OWf;           // full output grid (class mode)
+};
+
 // 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32.
-template <int MODE, int STRIDE, int WM, int WN, int TM, int TN, int NST>
-__global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsigned act_bytes, unsigned w_bytes) {
+template <int MODE, int WM, int WN, int TM, int TN, int NST>
+__global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPipeArgs ta) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int AR = BM / 64, BR = BN / 64;  // buffer-lds instructions per wave per tile (16 rows each)
@@ -50,13 +63,13 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsig
   const int mt = bid / nnt, nt = bid - mt * nnt;
   const int m0 = mt * BM, n0 = nt * BN;
 
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)act_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.wmat, (short)0, (int)w_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)ta.act_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.wmat, (short)0, (int)ta.w_bytes, 0x00020000);
 
   // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*16 + lane/4 ----
   const int lrow = lane >> 2, pchunk = lane & 3;
   unsigned a_off0[AR], a_mask[AR];
-  int a_py[AR], a_px[AR];
+  const int hw = p.OH * p.OW;
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int row = (wid * AR + i) * 16 + lrow;
@@ -64,41 +77,22 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsig
     const int m = m0 + row;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
-    const int hw = p.OH * p.OW;
     const int n = mm / hw, rem = mm - n * hw;
     const int oh = rem / p.OW, ow = rem - oh * p.OW;
-    int yb, xb;  // source coordinate of tap (0,0)
+    int yb, xb;  // source coordinate of the row origin; tap t reads (yb + tap_dy[t], xb + tap_dx[t])
     if (MODE == MODE_FWD) {
-      yb = oh * p.stride - p.pad;
-      xb = ow * p.stride - p.pad;
-    } else if (STRIDE == 1) {
-      yb = oh + p.pad;  // tap (r,s) reads y = yb - r
-      xb = ow + p.pad;
+      yb = oh * p.stride;
+      xb = ow * p.stride;
     } else {
-      a_py[i] = (oh + p.pad) & 1;
-      a_px[i] = (ow + p.pad) & 1;
-      yb = (oh + p.pad) >> 1;  // tap (r,s) valid iff r == py (mod 2); reads y = yb - (r - py)/2
-      xb = (ow + p.pad) >> 1;
+      yb = oh;  // class / stride-1 grids: displacements carry pad and parity
+      xb = ow;
     }
     unsigned mask = 0;
-    for (int r = 0; r < p.R; ++r)
-      for (int s = 0; s < p.S; ++s) {
-        int y, x;
-        bool v = ok;
-        if (MODE == MODE_FWD) {
-          y = yb + r;
-          x = xb + s;
-        } else if (STRIDE == 1) {
-          y = yb - r;
-          x = xb - s;
-        } else {
-          v = v && ((r & 1) == a_py[i]) && ((s & 1) == a_px[i]);
-          y = yb - ((r - a_py[i]) >> 1);
-          x = xb - ((s - a_px[i]) >> 1);
-        }
-        v = v && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
-        mask |= (v ? 1u : 0u) << (r * p.S + s);
-      }
+    for (int t = 0; t < ta.ntaps; ++t) {
+      const int y = yb + ta.tap_dy[t], x = xb + ta.tap_dx[t];
+      const bool v = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
+      mask |= (v ? 1u : 0u) << t;
+    }
     a_mask[i] = mask;
     a_off0[i] = (unsigned)(((long long)n * p.IH * p.IW + (long long)yb * p.IW + xb) * p.IC + lc * 8) * 2u;
   }
@@ -108,44 +102,31 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsig
     const int row = (wid * BR + i) * 16 + lrow;
     b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + ((pchunk ^ ((row >> 2) & 3)) * 8)) * 2);
   }
-  const int nkt = p.Kg / 32;
+  const int cpt = p.IC / 32;  // k-tiles per tap
+  const int nkt = ta.ntaps * cpt;
 
-  // incremental tap state of the next tile to issue (wave-uniform)
-  int it_r = 0, it_s = 0, it_c = 0, it_k = 0;
+  // incremental state of the next tile to issue (wave-uniform)
+  int it_t = 0, it_c = 0, it_k = 0;
   auto issue = [&](int stage) {
     char* As = smem + stage * STAGE;
     char* Bs = As + BM * 64;
     const bool live = it_k < nkt;
-    const int t = it_r * p.S + it_s;
-    int tapoff;  // byte offset of tap (r,s) channel block c relative to tap (0,0)
-    if (MODE == MODE_FWD)
-      tapoff = ((it_r * p.IW + it_s) * p.IC + it_c) * 2;
-    else
-      tapoff = (it_c - (it_r * p.IW + it_s) * p.IC) * 2;
+    const int t = live ? it_t : 0;
+    const int tapoff = ((ta.tap_dy[t] * p.IW + ta.tap_dx[t]) * p.IC + it_c) * 2;
+    const unsigned boff = (unsigned)((ta.tap_w[t] * p.IC + it_c) * 2);  // weight k offset (Kg = R*S*IC)
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      unsigned voff;
-      if (MODE == MODE_DGRAD && STRIDE == 2) {
-        const int dy = (it_r - a_py[i]) >> 1, dx = (it_s - a_px[i]) >> 1;
-        voff = a_off0[i] + (unsigned)((it_c - (dy * p.IW + dx) * p.IC) * 2);
-      } else {
-        voff = a_off0[i] + (unsigned)tapoff;
-      }
-      voff = (live && ((a_mask[i] >> t) & 1u)) ? voff : kOOB;
-      buf_lds16(rsa, As + (wid * AR + i) * 1024, voff);
+      const unsigned voff = a_off0[i] + (unsigned)tapoff;
+      buf_lds16(rsa, As + (wid * AR + i) * 1024, (live && ((a_mask[i] >> t) & 1u)) ? voff : kOOB);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
-      buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + (unsigned)(it_k * 64) : kOOB);
-    // advance
+      buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
     ++it_k;
     it_c += 32;
     if (it_c == p.IC) {
       it_c = 0;
-      if (++it_s == p.S) {
-        it_s = 0;
-        ++it_r;
-      }
+      ++it_t;
     }
   };
 
@@ -257,7 +238,14 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, unsig
     const int r = idx / CPR, cc = idx - r * CPR;
     if (r >= rows_valid) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
-    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
+    size_t orow = (size_t)(m0 + r);
+    if (ta.cls) {  // class row -> full output pixel (2h'+ph, 2w'+pw)
+      const int m = m0 + r;
+      const int n = m / hw, rem = m - n * hw;
+      const int oh = rem / p.OW, ow = rem - oh * p.OW;
+      orow = ((size_t)n * ta.OHf + 2 * oh + ta.ph) * ta.OWf + 2 * ow + ta.pw;
+    }
+    const size_t off = orow * p.Ng + n0 + cc * 8;
     if (p.add != nullptr) {
       const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
       unsigned* vv = reinterpret_cast<unsigned*>(&v);

@@ -1,0 +1,226 @@
+// wgrad ("TN") implicit GEMM, LDS-DMA pipeline (C % 8 == 0).  Included by conv_gemm.hip inside
+// namespace avt after conv_nt_pipe.h (uses GemmTNParams, buf_lds16, wait_vmcnt, kOOB).
+//
+//   DW[k_out][(r,s,c)] += sum_{pix} DY[pix][k_out] * X(pix; r,s,c)
+//
+// Both operands are pixel-major: a k-tile is 32 consecutive output pixels; the LDS images are
+// [32 pix][BM] and [32 pix][BN] bf16 with unpadded rows whose 16-B chunks are XOR-swizzled
+// (chunk ^ f(row)) so that the ds_read_b64_tr_b16 fragment reads are bank-conflict-free.  The
+// images are filled with `buffer_load_dwordx4 ... lds` (lane-linear; the swizzle goes on the
+// source chunk).  Each lane owns one fixed logical chunk (a fixed k_out block for DY, a fixed
+// (r,s,c) patch column block for X); per k-tile it decomposes its pixel(s) with magic-number
+// divisions.  NST-stage ring, NST-1 tiles in flight, split-K over blockIdx.y, fp32 atomics.
+#pragma once
+
+struct MagicDiv {  // exact floor(n / d) for 32-bit n (Granlund-Montgomery)
+  unsigned m, l;
+};
+
+static inline MagicDiv make_magic(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return MagicDiv{(unsigned)m, l};
+}
+
+__device__ __forceinline__ unsigned magic_div(unsigned n, MagicDiv md) {
+  if (md.l == 0) return n;  // d == 1
+  const unsigned t = __umulhi(md.m, n);
+  return (t + ((n - t) >> 1)) >> (md.l - 1);
+}
+
+struct GemmTNPipeParams {
+  GemmTNParams p;
+  MagicDiv div_pq, div_q;
+  unsigned dy_bytes, x_bytes;
+};
+
+template <int ROWB>
+__device__ __forceinline__ int tn_swz(int row) {  // chunk XOR for a row of ROWB bytes
+  return ROWB == 256 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
+}
+
+template <int WM, int WN, int TM, int TN, int NST>
+__global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  static_assert(BM == 64 || BM == 128, "BM");
+  static_assert(BN == 64 || BN == 128, "BN");
+  constexpr int AROWB = BM * 2, BROWB = BN * 2;          // bytes per pixel row
+  constexpr int A_RPI = 1024 / AROWB, B_RPI = 1024 / BROWB;  // rows per 1 KiB instruction
+  constexpr int AI = 32 / A_RPI / 4, BI = 32 / B_RPI / 4;    // instructions per wave per tile
+  constexpr int LPT = AI + BI;
+  constexpr int A_BYTES = 32 * AROWB, STAGE = 32 * (AROWB + BROWB);
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  const GemmTNParams& p = pp.p;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int nnt = p.Ng / BN;
+  const int ntiles = (p.Mg / BM) * nnt;
+  // 1-D grid of ntiles x splits, remapped so that each XCD runs a contiguous range: the tiles of
+  // one pixel range (split) share its DY/X rows through that XCD's L2
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / ntiles, tile = lin - split * ntiles;
+  const int mt = tile / nnt, nt = tile - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nkt_total = (p.Kred + 31) / 32;
+  const int kt_begin = split * p.kt_per_split;
+  const int kt_end = min(nkt_total, kt_begin + p.kt_per_split);
+  if (kt_begin >= kt_end) return;
+  const int nkt = kt_end - kt_begin;
+
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)pp.dy_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)pp.x_bytes, 0x00020000);
+
+  // A (dy) lanes: row-in-instruction and logical chunk (fixed per lane)
+  const int a_r = lane / (AROWB / 16), a_pc = lane % (AROWB / 16);
+  const int a_lc = a_pc ^ tn_swz<AROWB>(a_r);
+  const unsigned a_coff = (unsigned)((m0 + a_lc * 8) * 2);
+  // B (x gather) lanes
+  const int b_r = lane / (BROWB / 16), b_pc = lane % (BROWB / 16);
+  const int b_lc = b_pc ^ tn_swz<BROWB>(b_r);
+  const int col = n0 + b_lc * 8;
+  const int rs = col / p.Cp;
+  const int b_c = col - rs * p.Cp;
+  const int b_rr = rs / p.S, b_ss = rs - b_rr * p.S;
+  const bool b_colok = col < p.R * p.S * p.Cp;
+
+  // Per-slot pixel state, advanced incrementally by 32 pixels per tile (no divisions in the loop):
+  // 32 = step_oh*Q + step_ow; offsets use 24-bit multiplies (full-rate v_mul_u32_u24).
+  const int sh = p.stride - 1;
+  const unsigned rowB = (unsigned)(p.W * p.Cp * 2), pixB = (unsigned)(p.Cp * 2);
+  const unsigned imgB = (unsigned)(p.H * p.W * p.Cp * 2);
+  const int step_oh = 32 / p.Q, step_ow = 32 - (32 / p.Q) * p.Q;
+  const int y_off = b_rr - p.pad, x_off = b_ss - p.pad;
+  const unsigned cB = (unsigned)(b_c * 2);
+  int b_pix[BI], b_oh[BI], b_ow[BI];
+  unsigned b_nb[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wid * BI + i) * B_RPI + b_r;
+    const int pix = kt_begin * 32 + row;
+    const unsigned n = magic_div((unsigned)pix, pp.div_pq);
+    const unsigned rem = (unsigned)pix - n * (unsigned)(p.P * p.Q);
+    const unsigned oh = magic_div(rem, pp.div_q);
+    b_pix[i] = pix;
+    b_oh[i] = (int)oh;
+    b_ow[i] = (int)(rem - oh * (unsigned)p.Q);
+    b_nb[i] = n * imgB;
+  }
+  unsigned a_off[AI];
+  int a_pix[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wid * AI + i) * A_RPI + a_r;
+    a_pix[i] = kt_begin * 32 + row;
+    a_off[i] = (unsigned)a_pix[i] * (unsigned)(p.Mg * 2) + a_coff;
+  }
+  const unsigned a_step = 32u * (unsigned)(p.Mg * 2);
+
+  auto issue = [&](int kt, int stage) {  // tiles are issued in order; kt past the end is a dummy
+    char* As = smem + stage * STAGE;
+    char* Bs = As + A_BYTES;
+    const bool live = kt < kt_end;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const bool ok = live && a_pix[i] < p.Kred;
+      buf_lds16(rsa, As + (wid * AI + i) * 1024, ok ? a_off[i] : kOOB);
+      a_off[i] += a_step;
+      a_pix[i] += 32;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int y = (b_oh[i] << sh) + y_off, x = (b_ow[i] << sh) + x_off;
+      const bool ok = live && b_colok && b_pix[i] < p.Kred && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const unsigned off = b_nb[i] + __umul24((unsigned)y, rowB) + __umul24((unsigned)x, pixB) + cB;
+      const unsigned m = 0u - (unsigned)ok;  // branch-free select
+      buf_lds16(rsb, Bs + (wid * BI + i) * 1024, (off & m) | (kOOB & ~m));
+      b_pix[i] += 32;
+      b_ow[i] += step_ow;
+      b_oh[i] += step_oh;
+      if (b_ow[i] >= p.Q) {
+        b_ow[i] -= p.Q;
+        b_oh[i] += 1;
+      }
+      while (b_oh[i] >= p.P) {  // next image (more than once only when P*Q < 32)
+        b_oh[i] -= p.P;
+        b_nb[i] += imgB;
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  // tr-read lane geometry: group g = lane>>4 (16 lanes), t = lane&15 = 4q + pq
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, pq = t & 3;
+  const int tr_row = (g >> 1) * 8 + q;         // + 16*ks + 4*rr
+  const int tr_col = (g & 1) * 16 + 4 * pq;    // element column within a 32-wide fragment block
+  const int a_sw = tn_swz<AROWB>(q), b_sw = tn_swz<BROWB>(q);  // row & 3 == q for every read row
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(kt_begin + s, s);
+
+  for (int k = 0; k < nkt; ++k) {
+    wait_vmcnt<(NST - 2) * LPT>();
+    __builtin_amdgcn_s_barrier();
+    issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);
+    const char* As = smem + (k % NST) * STAGE;
+    const char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int c = wm * (BM / WM) + i * 32 + tr_col;
+        const int off = ((c >> 3) ^ a_sw) * 16 + (c & 7) * 2;
+        const char* a0 = As + (ks * 16 + tr_row) * AROWB + off;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * AROWB));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8, tmp);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * (BN / WN) + j * 32 + tr_col;
+        const int off = ((c >> 3) ^ b_sw) * 16 + (c & 7) * 2;
+        const char* b0 = Bs + (ks * 16 + tr_row) * BROWB + off;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * BROWB));
+        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bfr[j] = __builtin_bit_cast(bf16x8, tmp);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  wait_vmcnt<0>();
+
+  // ---- epilogue: fp32 atomics into DW[k_out][(r,s,c_real)] ----
+  const int ldw = p.R * p.S * p.Creal;
+  const int frow = lane & 31, fhalf = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cc = n0 + wn * (BN / WN) + j * 32 + frow;
+    const int crs = cc / p.Cp, c = cc - crs * p.Cp;
+    const bool cok = crs < p.R * p.S && c < p.Creal;
+    const int dcol = crs * p.Creal + c;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        if (cok && row < p.Mg) atomicAdd(p.dw + (size_t)row * ldw + dcol, acc[i][j][v]);
+      }
+  }
+}

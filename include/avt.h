@@ -46,6 +46,9 @@ int avt_bn_slots(void);
 /* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
+/* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
+ * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages) — an A/B knob */
+int avt_set_nt64_config(int cfg);
 /* wgrad split-K policy: about target_blocks blocks in total, at least min_ktiles 32-pixel tiles each */
 int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 size_t avt_bn_acc_doubles(int C);

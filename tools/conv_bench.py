@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--only", default="")
-    ap.add_argument("--wgrad-policy", default="512,16;1024,8;2048,4;256,32")
+    ap.add_argument("--wgrad-policy", default="1024,8")
+    ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -76,6 +77,19 @@ def main():
         acc = torch.zeros(16 * K * 3, device=dev, dtype=torch.float64)
         flops = 2.0 * N * Pq * Qq * K * C * R * R
         line = f"{name:12s} M={N * Pq * Qq:7d} N={K:4d} K={kg:5d}"
+        if args.nt64 and K == 64 or args.nt64 and C == 64:
+            for cfg in [int(s) for s in args.nt64.split(",")]:
+                call("avt_set_nt64_config", cfg)
+                call("avt_set_conv_variant", 1)
+                if K == 64:
+                    ms = timeit(lambda: call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st,
+                                             pad, kg, S()))
+                    line += f" | nt64[{cfg}] fwd {flops / ms / 1e9:6.0f}"
+                if C == 64:
+                    ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
+                                             pad, S()))
+                    line += f" nt64[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
+            call("avt_set_nt64_config", 1)
         for v in [int(s) for s in args.variants.split(",")]:
             call("avt_set_conv_variant", v)
             if "fwd" in kinds:
@@ -96,7 +110,7 @@ def main():
                                              S()))
                     line += f" wgrad[{tb},{mk}] {flops / ms / 1e9:6.0f}"
                     tot[("wgrad" + pol, v)] = tot.get(("wgrad" + pol, v), 0) + ms
-                call("avt_set_wgrad_policy", 512, 16)
+                call("avt_set_wgrad_policy", 1024, 8)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
