@@ -33,7 +33,8 @@ SIGNATURES = {
     "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
-    "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),
     "avt_bn_finalize": (_I, [_P, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
     "avt_bn_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "avt_bn_bwd_workspace": (_Z, [_L, _I]),

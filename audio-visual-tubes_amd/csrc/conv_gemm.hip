@@ -460,6 +460,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 static int g_nt64_config = 1;  // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
 static int g_wgrad_blocks = 1024;  // split-K policy of the wgrad kernel (tunable for A/B runs)
 static int g_wgrad_min_kt = 8;
+static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -634,42 +635,17 @@ extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const 
   return check_launch("conv2d_dgrad");
 }
 
-template <int CVEC, int BM, int BN>
-static void launch_tn(GemmTNParams p, hipStream_t st) {
-  const int tiles = (p.Mg / BM) * (p.Ng / BN);
-  const int nkt = (p.Kred + 31) / 32;
-  // ~2 resident blocks per CU in total, each with a long pixel (K) loop: the fp32 atomics of the
-  // split-K epilogue (BM*BN*4 bytes per block) stay a small fraction of the MFMA time
-  int splits = (g_wgrad_blocks + tiles - 1) / tiles;
-  int kps = (nkt + splits - 1) / splits;
-  if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;
-  splits = (nkt + kps - 1) / kps;
-  p.kt_per_split = kps;
-  if (CVEC == 8 && conv_variant() == 1) {
-    GemmTNPipeParams pp;
-    pp.p = p;
-    pp.div_pq = make_magic((unsigned)(p.P * p.Q));
-    pp.div_q = make_magic((unsigned)p.Q);
-    pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
-    pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
-    constexpr int TM = BM / 64, TN = BN / 64;
-    hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, TM, TN, 4>), dim3(tiles * splits), dim3(256), 0, st, pp);
-    return;
-  }
-  hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(tiles, splits), dim3(256), 0, st, p);
-}
+// wgrad launch plan: tile shape, split-K and (pipelined kernel) the fp32 partial slab it needs.
+struct WgradPlan {
+  GemmTNParams p;
+  int BM, BN, tiles, splits;
+  bool pipe;            // LDS-DMA pipelined kernel (C % 8 == 0) vs register-staged (stems)
+  size_t slab_bytes;    // splits * K * R*S*C * 4 when split-K partials go through a slab
+};
 
-// DW must be zero-initialised (or hold a gradient to accumulate into) by the caller.
-extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
-                                int K, int R, int S, int stride, int pad, void* stream) {
-  AVT_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
-  AVT_REQUIRE(K % 64 == 0, "conv2d_wgrad: K=%d must be a multiple of 64", K);
-  AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
-  AVT_REQUIRE(Creal <= Cp, "conv2d_wgrad: Creal > Cp");
-  GemmTNParams p{};
-  p.dy = (const bf16_t*)dy;
-  p.x = (const bf16_t*)x;
-  p.dw = dw;
+static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
+  WgradPlan pl{};
+  GemmTNParams& p = pl.p;
   p.Mg = K;
   p.H = H; p.W = W; p.Cp = Cp; p.Creal = Creal;
   p.P = conv_out(H, R, stride, pad);
@@ -677,18 +653,100 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
   p.Kred = N * p.P * p.Q;
   const int ncols = R * S * Cp;
+  pl.BN = (ncols % 128 == 0 || ncols > 128) ? 128 : 64;
+  pl.BM = (K % 128 == 0 && Cp % 8 == 0) || (K % 128 == 0 && Cp == 4) ? 128 : 64;
+  p.Ng = ((ncols + pl.BN - 1) / pl.BN) * pl.BN;
+  pl.tiles = (p.Mg / pl.BM) * (p.Ng / pl.BN);
+  const int nkt = (p.Kred + 31) / 32;
+  // at most g_wgrad_blocks blocks (a whole number of resident waves: 2 blocks per CU), each with
+  // a long pixel (K) loop
+  int splits = g_wgrad_blocks / pl.tiles;
+  if (splits < 1) splits = 1;
+  int kps = (nkt + splits - 1) / splits;
+  if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;
+  pl.splits = (nkt + kps - 1) / kps;
+  p.kt_per_split = kps;
+  pl.pipe = (Cp % 8 == 0) && conv_variant() == 1;
+  // slab + reduce pass for moderate split counts (measured faster on layer3/4); very deep splits
+  // (layer1/2: 100-200 splits of a small output) keep the fp32 atomics, which overlap the compute
+  pl.slab_bytes = (pl.pipe && pl.splits > 1 && pl.splits <= g_wgrad_slab_max)
+                      ? (size_t)pl.splits * K * R * S * Creal * sizeof(float)
+                      : 0;
+  return pl;
+}
+
+template <int CVEC, int BM, int BN>
+static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
+  GemmTNParams p = pl.p;
+  if (pl.pipe) {
+    GemmTNPipeParams pp;
+    pp.p = p;
+    pp.div_pq = make_magic((unsigned)(p.P * p.Q));
+    pp.div_q = make_magic((unsigned)p.Q);
+    pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
+    pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
+    pp.slab = slab;
+    constexpr int TM = BM / 64, TN = BN / 64;
+    hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, TM, TN, 4>), dim3(pl.tiles * pl.splits), dim3(256), 0, st, pp);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(pl.tiles, pl.splits), dim3(256), 0, st, p);
+}
+
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, long long n,
+                                                                float* __restrict__ dw) {
+  const long long nv = n / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a = reinterpret_cast<const f32x4*>(dw)[i];
+    for (int s = 0; s < splits; ++s) a += reinterpret_cast<const f32x4*>(slab + (size_t)s * n)[i];
+    reinterpret_cast<f32x4*>(dw)[i] = a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long i = nv * 4 + threadIdx.x;
+    float a = dw[i];
+    for (int s = 0; s < splits; ++s) a += slab[(size_t)s * n + i];
+    dw[i] = a;
+  }
+}
+
+extern "C" size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride,
+                                             int pad) {
+  return wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad).slab_bytes;
+}
+
+// dw += wgrad.  With a workspace of avt_conv2d_wgrad_workspace() bytes the split-K partials go
+// through an fp32 slab + one reduction pass (deterministic, 2x cheaper than atomics); without it
+// (or for the stems) they are added with fp32 atomics.  dw must hold zero or a gradient to add to.
+extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
+                                int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  AVT_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
+  AVT_REQUIRE(K % 64 == 0, "conv2d_wgrad: K=%d must be a multiple of 64", K);
+  AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
+  AVT_REQUIRE(Creal <= Cp, "conv2d_wgrad: Creal > Cp");
+  AVT_REQUIRE(Cp % 8 != 0 || Creal == Cp, "conv2d_wgrad: channel padding only for the stems");
+  WgradPlan pl = wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  pl.p.dy = (const bf16_t*)dy;
+  pl.p.x = (const bf16_t*)x;
+  pl.p.dw = dw;
+  float* slab = (pl.slab_bytes > 0 && workspace != nullptr && ws_bytes >= pl.slab_bytes) ? (float*)workspace : nullptr;
   hipStream_t st = (hipStream_t)stream;
-  const int BN = (ncols % 128 == 0 || ncols > 128) ? 128 : 64;
-  p.Ng = ((ncols + BN - 1) / BN) * BN;
-  const bool bm128 = (K % 128 == 0);
+  const int BM = pl.BM, BN = pl.BN;
   if (Cp == 4) {
-    if (bm128) launch_tn<4, 128, 128>(p, st); else launch_tn<4, 64, 128>(p, st);
+    if (BM == 128) launch_tn<4, 128, 128>(pl, slab, st); else launch_tn<4, 64, 128>(pl, slab, st);
   } else if (Cp == 1) {
-    if (BN == 128) launch_tn<1, 64, 128>(p, st); else launch_tn<1, 64, 64>(p, st);
+    if (BN == 128) launch_tn<1, 64, 128>(pl, slab, st); else launch_tn<1, 64, 64>(pl, slab, st);
   } else if (BN == 128) {
-    if (bm128) launch_tn<8, 128, 128>(p, st); else launch_tn<8, 64, 128>(p, st);
+    if (BM == 128) launch_tn<8, 128, 128>(pl, slab, st); else launch_tn<8, 64, 128>(pl, slab, st);
   } else {
-    if (bm128) launch_tn<8, 128, 64>(p, st); else launch_tn<8, 64, 64>(p, st);
+    if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
+  }
+  if (slab) {
+    const long long n = (long long)K * R * S * Creal;
+    long long blocks = (n / 4 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, pl.splits, n, dw);
   }
   return check_launch("conv2d_wgrad");
 }

@@ -33,6 +33,7 @@ struct GemmTNPipeParams {
   GemmTNParams p;
   MagicDiv div_pq, div_q;
   unsigned dy_bytes, x_bytes;
+  float* slab;  // non-null: store the split's partial tile to slab[split][Mg][R*S*C] (plain stores)
 };
 
 template <int ROWB>
@@ -206,21 +207,25 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
   }
   wait_vmcnt<0>();
 
-  // ---- epilogue: fp32 atomics into DW[k_out][(r,s,c_real)] ----
-  const int ldw = p.R * p.S * p.Creal;
+  // ---- epilogue: partial tile -> slab (plain stores) or fp32 atomics into DW[k_out][(r,s,c)] ----
+  const int ldw = p.R * p.S * p.Creal;  // Cp == Creal for this kernel
   const int frow = lane & 31, fhalf = lane >> 5;
+  float* dst = pp.slab ? pp.slab + (size_t)split * p.Mg * ldw : p.dw;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int cc = n0 + wn * (BN / WN) + j * 32 + frow;
-    const int crs = cc / p.Cp, c = cc - crs * p.Cp;
-    const bool cok = crs < p.R * p.S && c < p.Creal;
-    const int dcol = crs * p.Creal + c;
+    const bool cok = cc < ldw;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-        if (cok && row < p.Mg) atomicAdd(p.dw + (size_t)row * ldw + dcol, acc[i][j][v]);
+        if (cok && row < p.Mg) {
+          if (pp.slab)
+            dst[(size_t)row * ldw + cc] = acc[i][j][v];
+          else
+            atomicAdd(dst + (size_t)row * ldw + cc, acc[i][j][v]);
+        }
       }
   }
 }

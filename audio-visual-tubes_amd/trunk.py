@@ -241,9 +241,12 @@ class Trunk:
 
     def _wgrad(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
         dw = store.grad(spec.name)
+        wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+                        spec.stride, spec.pad))
+        ws = torch.empty(wsb, device=x.device, dtype=torch.uint8) if wsb else None
         ev = ConvProfiler.begin()
         call("avt_conv2d_wgrad", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
-             spec.stride, spec.pad, stream_ptr())
+             spec.stride, spec.pad, P(ws), wsb, stream_ptr())
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin)
 
     def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None):

@@ -57,9 +57,12 @@ int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, in
 /* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
 int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, void* stream);
-/* dw[K][R][S][Creal] += wgrad(x[N,H,W,Cp], dy[N,P,Q,K])  (fp32 atomics; caller zeroes dw) */
+/* dw[K][R][S][Creal] += wgrad(x[N,H,W,Cp], dy[N,P,Q,K]).  Split-K partials go through an fp32 slab
+ * in `workspace` (>= avt_conv2d_wgrad_workspace(...) bytes; deterministic) or, if it is NULL/too
+ * small or for the stems, are added with fp32 atomics. */
+size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad);
 int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
-                     int S, int stride, int pad, void* stream);
+                     int S, int stride, int pad, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- batch norm (train mode) ---- */
 /* merge bn_acc (see avt_conv2d_fwd) over `rows` rows -> scale, shift, mean, invstd (fp32 [C]);

@@ -156,7 +156,7 @@ def test_stem_fwd_wgrad(cin, cp, H, W):
     assert rel_err(y, ref) < 8e-3
     dy = _rand_act(N, Pq, Qq, K, 4)
     dw = torch.zeros(K, R, R, cin, device=DEV)
-    call("avt_conv2d_wgrad", P(xn), P(dy.to(DEV)), P(dw), N, H, W, cp, cin, K, R, R, st, pad, S())
+    wgrad(xn, dy.to(DEV), dw, N, H, W, cp, cin, K, R, st, pad)
     ref_dw = torch.nn.grad.conv2d_weight(xb, (K, cin, R, R), dy.double().permute(0, 3, 1, 2), stride=st, padding=pad)
     torch.cuda.synchronize()
     assert rel_err(dw.permute(0, 3, 1, 2), ref_dw) < 2e-4
@@ -184,18 +184,26 @@ def test_conv_dgrad(case):
     assert rel_err(dx2, ref + add.double()) < 8e-3
 
 
+def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
+    wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, cp, creal, K, R, R, st, pad)) if slab else 0
+    ws = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
+    call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, cp, creal, K, R, R, st, pad, P(ws) if slab else None, wsb,
+         S())
+
+
+@pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wgrad(case):
+def test_conv_wgrad(case, slab):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
     dy = _rand_act(N, Pq, Qq, K, 9)
-    dw = torch.zeros(K, R, R, C, device=DEV)
-    call("avt_conv2d_wgrad", P(x.to(DEV)), P(dy.to(DEV)), P(dw), N, H, W, C, C, K, R, R, st, pad, S())
+    dw = torch.full((K, R, R, C), 0.25, device=DEV)  # accumulates into an existing gradient
+    wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()
-    assert rel_err(dw.permute(0, 3, 1, 2), ref) < 2e-4
+    assert rel_err(dw.permute(0, 3, 1, 2) - 0.25, ref) < 2e-4
 
 
 def test_wgrad_large_splitk():
@@ -204,7 +212,7 @@ def test_wgrad_large_splitk():
     x = _rand_act(N, H, W, C, 10).relu()
     dy = _rand_act(N, H, W, K, 11)
     dw = torch.zeros(K, R, R, C, device=DEV)
-    call("avt_conv2d_wgrad", P(x.to(DEV)), P(dy.to(DEV)), P(dw), N, H, W, C, C, K, R, R, st, pad, S())
+    wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()

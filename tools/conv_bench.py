@@ -9,7 +9,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import avtubes  # noqa: E402,F401
-from avt_amd._lib import call  # noqa: E402
+from avt_amd._lib import call, query  # noqa: E402
 
 # (name, H, W, C, K, R, stride, pad)
 SHAPES = [
@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--wgrad-policy", default="1024,8")
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
+    ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -106,8 +107,10 @@ def main():
                 for pol in args.wgrad_policy.split(";"):
                     tb, mk = (int(s) for s in pol.split(","))
                     call("avt_set_wgrad_policy", tb, mk)
+                    wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+                    ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
                     ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st, pad,
-                                             S()))
+                                             P(ws), wsb if args.slab else 0, S()))
                     line += f" wgrad[{tb},{mk}] {flops / ms / 1e9:6.0f}"
                     tot[("wgrad" + pol, v)] = tot.get(("wgrad" + pol, v), 0) + ms
                 call("avt_set_wgrad_policy", 1024, 8)
