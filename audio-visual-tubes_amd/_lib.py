@@ -30,6 +30,8 @@ SIGNATURES = {
     "avt_set_conv_variant": (_I, [_I]),
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
+    "avt_set_nt128_config": (_I, [_I]),
+    "avt_set_wgrad_slab_max": (_I, [_I, _I]),
     "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
@@ -39,6 +41,9 @@ SIGNATURES = {
     "avt_bn_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "avt_bn_bwd_workspace": (_Z, [_L, _I]),
     "avt_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_bn_relu_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_stem_bn_relu_maxpool_fwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
+    "avt_stem_maxpool_bn_relu_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P]),
     "avt_maxpool3s2_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "avt_maxpool3s2_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "avt_audio_pool_norm_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _P]),

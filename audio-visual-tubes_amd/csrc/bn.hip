@@ -10,6 +10,9 @@
 //   bwd : bn_bwd_reduce adds per-block (sum g', sum g'*xhat) (g' = g*[y>0]) into an fp64
 //         accumulator [AVT_BN_SLOTS][C][2] -> bn_bwd_finalize (dgamma, dbeta, k1, k2; re-zeroes) ->
 //         bn_bwd_apply: g_c = gamma*invstd*(g' - k1 - xhat*k2).
+//         avt_bn_relu_bwd recomputes the ReLU mask from (xc, scale, shift) instead of reading y
+//         (BasicBlock.bn1, base_models.py:47-48); the stem's bn1+relu+maxpool is fused both ways
+//         (avt_stem_*, below) so its full-resolution activation is never stored.
 #include "avt_common.h"
 
 namespace avt {
@@ -69,6 +72,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ a
 }
 
 // out = [relu]( x*scale + shift + [residual*rscale + rshift | residual] )
+// The channel block of vector i is i % (C/8); POW2 (C/8 a power of two) takes it as a bit mask.
+// The per-channel constants are re-read every iteration (L1 hits): hoisting them costs enough
+// VGPRs to drop occupancy, which this HBM-bound loop needs more.
+template <bool POW2>
+__device__ __forceinline__ int chan_block(long long i, int cv) {
+  return POW2 ? (int)((unsigned)i & (unsigned)(cv - 1)) : (int)(i % cv);
+}
+
+template <bool POW2>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, const float* __restrict__ rscale,
@@ -76,11 +88,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                        long long nvec, int C, int relu) {
   const int cv = C / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
+    const int c0 = chan_block<POW2>(i, cv) * 8;
     float f[8];
     unpack8(reinterpret_cast<const u32x4*>(x)[i], f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = f[e] * scale[c0 + e] + shift[c0 + e];
+    for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], scale[c0 + e], shift[c0 + e]);
     if (res) {
       float r[8];
       unpack8(reinterpret_cast<const u32x4*>(res)[i], r);
@@ -100,9 +112,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// ReLU mask of the backward pass.  Either read from the saved output y (y > 0) or recomputed
+// from the pre-activation: relu(fma(xc, mscale, mshift)) > 0 -- the exact expression bn_apply
+// evaluated in the forward, so the mask is identical without re-reading y.
+__device__ __forceinline__ void relu_mask8(float* gg, const float* xx, const bf16_t* __restrict__ y, size_t off,
+                                           const float* __restrict__ mscale, const float* __restrict__ mshift,
+                                           int c0) {
+  if (y) {
+    float yy[8];
+    unpack8(reinterpret_cast<const u32x4*>(y)[off], yy);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
+  } else if (mscale) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gg[e] = __builtin_fmaf(xx[e], mscale[c0 + e], mshift[c0 + e]) > 0.f ? gg[e] : 0.f;
+  }
+}
+
 // Per-block sums of g' and g'*xhat added into acc[block % SLOTS][C][2].  Block: 256 threads; a
 // thread owns channel chunk (tid % (C/8)) and walks rows tid/(C/8) + k*(256/(C/8)).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                                            const float* __restrict__ mscale,
+                                                            const float* __restrict__ mshift,
                                                             const bf16_t* __restrict__ xc, const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, double* __restrict__ acc,
                                                             long long rows, int C, int rows_per_block) {
@@ -125,12 +156,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     float gg[8], xx[8];
     unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
     unpack8(reinterpret_cast<const u32x4*>(xc)[off], xx);
-    if (y) {
-      float yy[8];
-      unpack8(reinterpret_cast<const u32x4*>(y)[off], yy);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
-    }
+    relu_mask8(gg, xx, y, off, mscale, mshift, c0);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       s1[e] += gg[e];
@@ -176,7 +202,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
+template <bool POW2>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
+                                                           const float* __restrict__ mscale,
+                                                           const float* __restrict__ mshift,
                                                            const bf16_t* __restrict__ xc, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
                                                            const float* __restrict__ gamma, const float* __restrict__ k1,
@@ -184,16 +213,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
                                                            bf16_t* __restrict__ gmask_out, long long nvec, int C) {
   const int cv = C / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
-    const int c0 = (int)(i % cv) * 8;
+    const int c0 = chan_block<POW2>(i, cv) * 8;
     float gg[8], xx[8], o[8];
     unpack8(reinterpret_cast<const u32x4*>(g)[i], gg);
     unpack8(reinterpret_cast<const u32x4*>(xc)[i], xx);
-    if (y) {
-      float yy[8];
-      unpack8(reinterpret_cast<const u32x4*>(y)[i], yy);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
-    }
+    relu_mask8(gg, xx, y, (size_t)i, mscale, mshift, c0);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int c = c0 + e;
@@ -210,6 +234,123 @@ static int ew_grid(long long nvec) {
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
   return (int)b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stem: bn1 -> relu -> MaxPool2d(3,2,1) (models/base_models.py:200-203) without materialising the
+// full-resolution activation h0 = relu(bn(c0)), the largest tensor of either trunk.
+//   fwd : one thread per (pooled pixel, 8 channels) evaluates h0 on its 3x3 window exactly as
+//         bn_apply would (fma, relu, bf16 round), keeps the first max, and writes the pooled value,
+//         the window argmax and carg = c0 at the argmax (the only pre-activations the backward's
+//         reduction needs).
+//   bwd : g'(h,w) = [h0(h,w) > 0] * sum of gy over the windows whose argmax is (h,w).  Its two
+//         BN reductions (sum g', sum g'*xhat) are taken over the pooled grid from (gy, carg) --
+//         a position picked by several windows contributes once per window, which sums to the
+//         same total -- and the apply pass gathers g' per input pixel like maxpool3s2_bwd.
+// One block per output row (n, p) [fwd] / input row (n, h) [bwd]; the block's threads stride over
+// that row's (column, 8-channel block) items; cv = C/8 = 1 << cvs.
+__global__ __launch_bounds__(256) void stem_bn_relu_maxpool_fwd_kernel(
+    const bf16_t* __restrict__ c, const float* __restrict__ scale, const float* __restrict__ shift,
+    bf16_t* __restrict__ y, unsigned char* __restrict__ idx, bf16_t* __restrict__ carg, int H, int W, int C, int cvs,
+    int P, int Q) {
+  const int row = blockIdx.x;  // n * P + p
+  const int n = row / P, p = row - n * P;
+  const int cv = 1 << cvs;
+  const int r_lo = p == 0 ? 1 : 0, r_hi = min(2, H - 1 - (2 * p - 1));
+  const bf16_t* cimg = c + (size_t)n * H * W * C;
+  for (int t = threadIdx.x; t < Q * cv; t += 256) {
+    const int q = t >> cvs, c8 = t & (cv - 1);
+    float sc[8], sh[8], best[8], bc[8];
+    int bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = scale[c8 * 8 + e];
+      sh[e] = shift[c8 * 8 + e];
+      best[e] = -INFINITY;
+      bc[e] = 0.f;
+      bi[e] = 0;
+    }
+    for (int r = r_lo; r <= r_hi; ++r) {
+      const int h = p * 2 - 1 + r;
+      for (int s = 0; s < 3; ++s) {
+        const int w = q * 2 - 1 + s;
+        if (w < 0 || w >= W) continue;
+        float xv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(cimg + ((size_t)h * W + w) * C + c8 * 8), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f(f2bf(fmaxf(__builtin_fmaf(xv[e], sc[e], sh[e]), 0.f)));
+          if (f > best[e] || f != f) {
+            best[e] = f;
+            bc[e] = xv[e];
+            bi[e] = r * 3 + s;
+          }
+        }
+      }
+    }
+    const size_t off = ((size_t)row * Q + q) * C + c8 * 8;
+    *reinterpret_cast<u32x4*>(y + off) = pack8(best);
+    *reinterpret_cast<u32x4*>(carg + off) = pack8(bc);
+    unsigned long long ib = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ib |= (unsigned long long)bi[e] << (8 * e);
+    *reinterpret_cast<unsigned long long*>(idx + off) = ib;
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ gy, const unsigned char* __restrict__ idx, const bf16_t* __restrict__ c,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ k1,
+    const float* __restrict__ k2, bf16_t* __restrict__ gc, int H, int W, int C, int cvs, int P, int Q) {
+  const int row = blockIdx.x;  // n * H + h
+  const int n = row / H, h = row - n * H;
+  const int cv = 1 << cvs;
+  // pooled rows p with 2p-1 <= h <= 2p+1, and the window row kh = h - (2p-1) in each
+  const int p_lo = h >> 1, p_hi = min(P - 1, (h + 1) >> 1);
+  for (int t = threadIdx.x; t < W * cv; t += 256) {
+    const int w = t >> cvs, c8 = t & (cv - 1);
+    float gg[8], xx[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gg[e] = 0.f;
+    const int q_lo = w >> 1, q_hi = min(Q - 1, (w + 1) >> 1);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int kh = h - (2 * p - 1);
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int pos = kh * 3 + (w - (2 * q - 1));
+        const size_t off = (((size_t)n * P + p) * Q + q) * C + c8 * 8;
+        const unsigned long long ib = *reinterpret_cast<const unsigned long long*>(idx + off);
+        float gv[8];
+        unpack8(*reinterpret_cast<const u32x4*>(gy + off), gv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if ((int)((ib >> (8 * e)) & 0xff) == pos) gg[e] += gv[e];
+      }
+    }
+    const size_t xo = ((size_t)row * W + w) * C + c8 * 8;
+    unpack8(*reinterpret_cast<const u32x4*>(c + xo), xx);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ch = c8 * 8 + e;
+      gg[e] = __builtin_fmaf(xx[e], scale[ch], shift[ch]) > 0.f ? gg[e] : 0.f;
+      const float xh = (xx[e] - mean[ch]) * invstd[ch];
+      o[e] = gamma[ch] * invstd[ch] * (gg[e] - k1[ch] - xh * k2[ch]);
+    }
+    *reinterpret_cast<u32x4*>(gc + xo) = pack8(o);
+  }
+}
+
+static void bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* mscale, const float* mshift,
+                                 const bf16_t* xc, const float* mean, const float* invstd, double* acc, long long rows,
+                                 int C, hipStream_t st) {
+  // ~2 blocks per CU of rows
+  long long rpb = (rows + 511) / 512;
+  const int rstep = 256 / (C / 8);
+  rpb = ((rpb + rstep - 1) / rstep) * rstep;
+  if (rpb < rstep) rpb = rstep;
+  const int nblk = (int)((rows + rpb - 1) / rpb);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, st, g, y, mscale, mshift, xc, mean, invstd, acc,
+                     rows, C, (int)rpb);
 }
 
 }  // namespace avt
@@ -236,8 +377,13 @@ extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shif
   AVT_REQUIRE((rscale == nullptr) == (rshift == nullptr), "bn_apply: rscale/rshift must be both set or both null");
   const long long nvec = rows * C / 8;
   if (nvec == 0) return AVT_OK;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                     scale, shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
+  const int grid = ew_grid(nvec);
+  if (256 % (C / 8) == 0)
+    hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, scale,
+                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, scale,
+                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
   return check_launch("bn_apply");
 }
 
@@ -258,18 +404,77 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  // ~2 blocks per CU of rows
-  long long rpb = (rows + 511) / 512;
-  const int rstep = 256 / (C / 8);
-  rpb = ((rpb + rstep - 1) / rstep) * rstep;
-  if (rpb < rstep) rpb = rstep;
-  const int nblk = (int)((rows + rpb - 1) / rpb);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
-                     (const bf16_t*)xc, mean, invstd, acc, rows, C, (int)rpb);
+  bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
+                       rows, C, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
-                     (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc, (bf16_t*)gmask_out, nvec, C);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
+                     nullptr, nullptr, (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc,
+                     (bf16_t*)gmask_out, nvec, C);
   return check_launch("bn_bwd");
+}
+
+// BN + ReLU backward with the mask recomputed from the pre-activation xc and the forward's
+// (scale, shift): y is never read.  Same workspace contract as avt_bn_bwd.
+extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale, const float* shift,
+                               const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                               void* gc, void* workspace, long long rows, int C, void* stream) {
+  AVT_REQUIRE(g && xc && scale && shift && mean && invstd && gamma && gc && workspace, "bn_relu_bwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn_relu_bwd: C=%d unsupported", C);
+  AVT_REQUIRE(rows > 0, "bn_relu_bwd: empty input");
+  AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_relu_bwd: workspace must be 8-byte aligned");
+  double* acc = (double*)workspace;
+  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k2 = k1 + C;
+  hipStream_t st = (hipStream_t)stream;
+  bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
+  const long long nvec = rows * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, nullptr, scale,
+                     shift, (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc, nullptr, nvec, C);
+  return check_launch("bn_relu_bwd");
+}
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+extern "C" int avt_stem_bn_relu_maxpool_fwd(const void* c, const float* scale, const float* shift, void* y, void* idx,
+                                            void* carg, int N, int H, int W, int C, void* stream) {
+  AVT_REQUIRE(c && scale && shift && y && idx && carg, "stem_bn_relu_maxpool_fwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "stem_bn_relu_maxpool_fwd: C=%d unsupported", C);
+  AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_bn_relu_maxpool_fwd: empty input");
+  const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(stem_bn_relu_maxpool_fwd_kernel, dim3(N * P), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)c, scale, shift, (bf16_t*)y, (unsigned char*)idx, (bf16_t*)carg, H, W, C,
+                     ilog2(C / 8), P, Q);
+  return check_launch("stem_bn_relu_maxpool_fwd");
+}
+
+extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, const void* carg, const void* c,
+                                            const float* scale, const float* shift, const float* mean,
+                                            const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                                            void* gc, void* workspace, int N, int H, int W, int C, void* stream) {
+  AVT_REQUIRE(gy && idx && carg && c && scale && shift && mean && invstd && gamma && gc && workspace,
+              "stem_maxpool_bn_relu_bwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "stem_maxpool_bn_relu_bwd: C=%d unsupported", C);
+  AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_maxpool_bn_relu_bwd: empty input");
+  AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");
+  const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
+  double* acc = (double*)workspace;
+  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k2 = k1 + C;
+  hipStream_t st = (hipStream_t)stream;
+  bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
+                       (long long)N * P * Q, C, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C,
+                     1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
+  hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), 0, st, (const bf16_t*)gy,
+                     (const unsigned char*)idx, (const bf16_t*)c, scale, shift, mean, invstd, gamma, k1, k2,
+                     (bf16_t*)gc, H, W, C, ilog2(C / 8), P, Q);
+  return check_launch("stem_maxpool_bn_relu_bwd");
 }

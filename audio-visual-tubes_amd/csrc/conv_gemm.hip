@@ -457,10 +457,23 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_nt_pipe.h"
 #include "conv_tn_pipe.h"
 
-static int g_nt64_config = 1;  // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
-static int g_wgrad_blocks = 1024;  // split-K policy of the wgrad kernel (tunable for A/B runs)
-static int g_wgrad_min_kt = 8;
+static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
+static int g_nt128_config = 0;  // ... and for GEMM N % 128 == 0
+static int g_wgrad_blocks = 0;     // wgrad split-K: 0 = wave model (wgrad_plan), >0 = fixed block target
+static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
+static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int d = 0;
+    hipDeviceProp_t pr;
+    n = (hipGetDevice(&d) == hipSuccess && hipGetDeviceProperties(&pr, d) == hipSuccess && pr.multiProcessorCount > 0)
+            ? pr.multiProcessorCount
+            : 256;
+  }
+  return n;
+}
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -480,15 +493,28 @@ extern "C" int avt_set_conv_variant(int v) {
 }
 
 extern "C" int avt_set_nt64_config(int cfg) {
-  AVT_REQUIRE(cfg >= 0 && cfg <= 3, "set_nt64_config: cfg in 0..3");
+  AVT_REQUIRE(cfg >= 0 && cfg <= 6, "set_nt64_config: cfg in 0..6");
   g_nt64_config = cfg;
   return AVT_OK;
 }
 
+extern "C" int avt_set_nt128_config(int cfg) {
+  AVT_REQUIRE(cfg >= 0 && cfg <= 4, "set_nt128_config: cfg=%d out of range", cfg);
+  avt::g_nt128_config = cfg;
+  return AVT_OK;
+}
+
 extern "C" int avt_set_wgrad_policy(int target_blocks, int min_ktiles) {
-  AVT_REQUIRE(target_blocks >= 1 && min_ktiles >= 1, "set_wgrad_policy: bad arguments");
+  AVT_REQUIRE(target_blocks >= 0 && min_ktiles >= 1, "set_wgrad_policy: bad arguments");
   avt::g_wgrad_blocks = target_blocks;
   avt::g_wgrad_min_kt = min_ktiles;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_wgrad_slab_max(int max_splits, int wave_cost) {
+  AVT_REQUIRE(max_splits >= 0 && wave_cost >= 0, "set_wgrad_slab_max: bad arguments");
+  avt::g_wgrad_slab_max = max_splits;
+  avt::g_wgrad_wave_cost = wave_cost;
   return AVT_OK;
 }
 
@@ -497,18 +523,22 @@ extern "C" int avt_set_wgrad_policy(int target_blocks, int min_ktiles) {
 // ------------------------------------------------------------------------------------------------
 static inline int conv_out(int in, int k, int st, int pad) { return (in + 2 * pad - k) / st + 1; }
 
-template <int MODE, int WM, int WN, int TM, int TN, int NST>
+template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK>
 static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgs& ta, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
   if (grid > 0)
-    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST>), dim3(grid), dim3(256), 0, st, p, ta);
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK>), dim3(grid), dim3(256), 0, st, p, ta);
 }
 
 // Builds the tap list(s) and launches: fwd / stride-1 dgrad in one launch; a stride-2 dgrad as
 // four parity-class launches, each walking only its class's taps.
-template <int MODE, int WM, int WN, int TM, int TN, int NST = 4>
+template <int MODE, int WM, int WN, int TM, int TN, int NST = 4, int BK = 32>
 static void launch_glds(const GemmNTParams& p, hipStream_t st) {
+  if (BK == 64 && p.IC % 64 != 0) {  // a 64-deep k-tile needs whole 64-channel taps
+    launch_glds<MODE, WM, WN, TM, TN, (NST > 3 ? NST : 3), 32>(p, st);
+    return;
+  }
   NTPipeArgs ta{};
   const int batch = p.M / (p.OH * p.OW);
   ta.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * p.IC * 2);
@@ -522,7 +552,7 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
         ta.tap_dy[t] = MODE == MODE_FWD ? r - p.pad : p.pad - r;
         ta.tap_dx[t] = MODE == MODE_FWD ? s - p.pad : p.pad - s;
       }
-    launch_pipe_one<MODE, WM, WN, TM, TN, NST>(p, ta, st);
+    launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(p, ta, st);
     return;
   }
   ta.cls = 1;
@@ -548,7 +578,7 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
       pc.M = batch * pc.OH * pc.OW;
       // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) still runs with an
       // empty K loop: its rows are written as 0 (+ add)
-      launch_pipe_one<MODE, WM, WN, TM, TN, NST>(pc, tc, st);
+      launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
     }
 }
 
@@ -556,12 +586,21 @@ template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
   if (CVEC == 8 && conv_variant() == 1) {
     if (p.Ng % 128 == 0) {
-      launch_glds<MODE, 2, 2, 2, 2>(p, st);  // 128 x 128
+      switch (g_nt128_config) {
+        case 1: launch_glds<MODE, 2, 2, 2, 2, 2, 64>(p, st); break;  // 128 x 128, k64, 2 stages
+        case 2: launch_glds<MODE, 2, 2, 2, 2, 3, 64>(p, st); break;  // 128 x 128, k64, 3 stages
+        case 3: launch_glds<MODE, 2, 2, 4, 2, 3>(p, st); break;      // 256 x 128, k32, 3 stages
+        case 4: launch_glds<MODE, 2, 2, 4, 2, 2, 64>(p, st); break;  // 256 x 128, k64, 2 stages
+        default: launch_glds<MODE, 2, 2, 2, 2>(p, st); break;        // 128 x 128, k32, 4 stages
+      }
     } else {  // 64-wide N (layer1 / stem-fed convs)
       switch (g_nt64_config) {
         case 0: launch_glds<MODE, 4, 1, 2, 2, 4>(p, st); break;  // 256 x 64, 4 stages
         case 2: launch_glds<MODE, 2, 2, 2, 1, 4>(p, st); break;  // 128 x 64, 4 stages
         case 3: launch_glds<MODE, 4, 1, 2, 2, 2>(p, st); break;  // 256 x 64, 2 stages
+        case 4: launch_glds<MODE, 2, 2, 2, 1, 3, 64>(p, st); break;  // 128 x 64, k64, 3 stages
+        case 5: launch_glds<MODE, 4, 1, 2, 2, 2, 64>(p, st); break;  // 256 x 64, k64, 2 stages
+        case 6: launch_glds<MODE, 2, 2, 2, 1, 2, 64>(p, st); break;  // 128 x 64, k64, 2 stages
         default: launch_glds<MODE, 2, 2, 2, 1, 3>(p, st); break;  // 128 x 64, 3 stages
       }
     }
@@ -658,9 +697,30 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   p.Ng = ((ncols + pl.BN - 1) / pl.BN) * pl.BN;
   pl.tiles = (p.Mg / pl.BM) * (p.Ng / pl.BN);
   const int nkt = (p.Kred + 31) / 32;
-  // at most g_wgrad_blocks blocks (a whole number of resident waves: 2 blocks per CU), each with
-  // a long pixel (K) loop
-  int splits = g_wgrad_blocks / pl.tiles;
+  // Split-K count.  The grid runs in "waves" of resident blocks (CUs x blocks per CU, set by the
+  // NST=4 ring's LDS: 256*(BM+BN) bytes per block).  For w = 1..4 waves take the largest split
+  // count that fits, s_w = floor(w*slots/tiles), and keep the one with the least
+  // w * (ceil(nkt/s_w) + wave_cost) -- k-tiles per block plus its fixed prologue/epilogue cost.
+  int splits;
+  if (g_wgrad_blocks > 0) {
+    splits = g_wgrad_blocks / pl.tiles;
+  } else {
+    const int occ = max(1, 163840 / (256 * (pl.BM + pl.BN)));
+    const long long slots = (long long)num_cus() * occ;
+    long long best = -1;
+    splits = 1;
+    for (int w = 1; w <= 4; ++w) {
+      const int s_w = (int)(w * slots / pl.tiles);
+      if (s_w < 1) continue;
+      const int kps_w = max(g_wgrad_min_kt, (nkt + s_w - 1) / s_w);
+      const long long waves = (((long long)pl.tiles * ((nkt + kps_w - 1) / kps_w)) + slots - 1) / slots;
+      const long long cost = waves * (kps_w + g_wgrad_wave_cost);
+      if (best < 0 || cost < best) {
+        best = cost;
+        splits = s_w;
+      }
+    }
+  }
   if (splits < 1) splits = 1;
   int kps = (nkt + splits - 1) / splits;
   if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;

@@ -41,14 +41,27 @@ struct NTPipeArgs {
   int OHf, OWf;           // full output grid (class mode)
 };
 
-// 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32.
-template <int MODE, int WM, int WN, int TM, int TN, int NST>
+// byte offset of 16-B chunk `chunk` of row `row` in a [rows][RB bytes] LDS image: the chunk is
+// XOR-swizzled by the row so that the 32 rows of an MFMA fragment read hit distinct banks
+template <int RB>
+__device__ __forceinline__ int swz_rb(int row, int chunk) {
+  if (RB == 64) return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+// 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32; BK = k-tile
+// depth (32 or 64 bf16: 64-B or whole 128-B lines per gathered row and tap).
+template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32>
 __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPipeArgs ta) {
   static_assert(WM * WN == 4, "4 waves");
+  static_assert(BK == 32 || BK == 64, "BK");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int AR = BM / 64, BR = BN / 64;  // buffer-lds instructions per wave per tile (16 rows each)
+  constexpr int RB = BK * 2;                 // bytes per LDS row
+  constexpr int CPR = RB / 16;               // 16-B chunks per row
+  constexpr int RPI = 1024 / RB;             // rows per 1 KiB buffer-lds instruction
+  constexpr int AR = BM / (4 * RPI), BR = BN / (4 * RPI);  // instructions per wave per tile
   constexpr int LPT = AR + BR;
-  constexpr int STAGE = (BM + BN) * 64;
+  constexpr int STAGE = (BM + BN) * RB;
   constexpr int CT_LD = BN + 8;
   constexpr int EPI_BYTES = BM * CT_LD * 2;
   constexpr int SMEM = (NST * STAGE > EPI_BYTES ? NST * STAGE : EPI_BYTES);
@@ -66,14 +79,14 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)ta.act_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.wmat, (short)0, (int)ta.w_bytes, 0x00020000);
 
-  // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*16 + lane/4 ----
-  const int lrow = lane >> 2, pchunk = lane & 3;
+  // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*RPI + lane/CPR ----
+  const int lrow = lane / CPR, pchunk = lane % CPR;
   unsigned a_off0[AR], a_mask[AR];
   const int hw = p.OH * p.OW;
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    const int row = (wid * AR + i) * 16 + lrow;
-    const int lc = pchunk ^ ((row >> 2) & 3);
+    const int row = (wid * AR + i) * RPI + lrow;
+    const int lc = RB == 64 ? (pchunk ^ ((row >> 2) & 3)) : (pchunk ^ ((row >> 1) & 7));
     const int m = m0 + row;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
@@ -99,17 +112,18 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
   unsigned b_off[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
-    const int row = (wid * BR + i) * 16 + lrow;
-    b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + ((pchunk ^ ((row >> 2) & 3)) * 8)) * 2);
+    const int row = (wid * BR + i) * RPI + lrow;
+    const int lc = RB == 64 ? (pchunk ^ ((row >> 2) & 3)) : (pchunk ^ ((row >> 1) & 7));
+    b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
   }
-  const int cpt = p.IC / 32;  // k-tiles per tap
+  const int cpt = p.IC / BK;  // k-tiles per tap
   const int nkt = ta.ntaps * cpt;
 
   // incremental state of the next tile to issue (wave-uniform)
   int it_t = 0, it_c = 0, it_k = 0;
   auto issue = [&](int stage) {
     char* As = smem + stage * STAGE;
-    char* Bs = As + BM * 64;
+    char* Bs = As + BM * RB;
     const bool live = it_k < nkt;
     const int t = live ? it_t : 0;
     const int tapoff = ((ta.tap_dy[t] * p.IW + ta.tap_dx[t]) * p.IC + it_c) * 2;
@@ -123,7 +137,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
     for (int i = 0; i < BR; ++i)
       buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
     ++it_k;
-    it_c += 32;
+    it_c += BK;
     if (it_c == p.IC) {
       it_c = 0;
       ++it_t;
@@ -147,19 +161,19 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
     __builtin_amdgcn_s_barrier();
     issue((kt + NST - 1) % NST);  // the stage read in iteration kt-1; every wave has passed that
     const char* As = smem + (kt % NST) * STAGE;
-    const char* Bs = As + BM * 64;
+    const char* Bs = As + BM * RB;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * (BM / WM) + i * 32 + frow;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz64(row, ks * 2 + fhalf));
+        af[i] = *reinterpret_cast<const bf16x8*>(As + swz_rb<RB>(row, ks * 2 + fhalf));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * (BN / WN) + j * 32 + frow;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(row, ks * 2 + fhalf));
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz_rb<RB>(row, ks * 2 + fhalf));
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -233,9 +247,9 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
         Ct[r * CT_LD + c] = f2bf(acc[i][j][v]);
       }
   __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int idx = tid; idx < BM * CPR; idx += 256) {
-    const int r = idx / CPR, cc = idx - r * CPR;
+  constexpr int OCPR = BN / 8;
+  for (int idx = tid; idx < BM * OCPR; idx += 256) {
+    const int r = idx / OCPR, cc = idx - r * OCPR;
     if (r >= rows_valid) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
     size_t orow = (size_t)(m0 + r);

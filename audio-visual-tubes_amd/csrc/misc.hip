@@ -84,7 +84,7 @@ __global__ void pack_dgrad_kernel(const float* __restrict__ w, bf16_t* __restric
   }
 }
 
-// Batched packing of many conv weights in one launch: blockIdx.y = conv index.
+// Batched packing of many conv weights (one fwd + one dgrad launch): blockIdx.y = conv index.
 struct PackDesc {
   const float* w;   // [K][R][S][C] fp32
   bf16_t* fwd;      // [K][Kg] or null
@@ -92,23 +92,59 @@ struct PackDesc {
   int K, RS, C, Cp, Kg, pad_;
 };
 
-__global__ __launch_bounds__(256) void pack_batched_kernel(const PackDesc* __restrict__ descs) {
+// fwd image [K][Kg] (rows zero-padded from R*S*Cp to Kg, channels from C to Cp).  The common case
+// (Cp == C, Kg == R*S*C) is a contiguous fp32 -> bf16 copy, 8 elements (2 x 16 B in, 16 B out) per
+// thread; the stems take the scalar path.
+__global__ __launch_bounds__(256) void pack_fwd_batched_kernel(const PackDesc* __restrict__ descs) {
   const PackDesc d = descs[blockIdx.y];
-  const long long nf = d.fwd ? (long long)d.K * d.Kg : 0;
-  const long long nd = d.dgrad ? (long long)d.K * d.RS * d.C : 0;
-  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < nf + nd; t += (long long)gridDim.x * blockDim.x) {
-    if (t < nf) {
-      const int k = (int)(t / d.Kg), col = (int)(t % d.Kg);
-      const int rs = col / d.Cp, c = col % d.Cp;
+  if (!d.fwd) return;
+  const int row = d.RS * d.C;
+  const int total = d.K * d.Kg;
+  const int tid = blockIdx.x * 256 + threadIdx.x, nthr = gridDim.x * 256;
+  if (d.Cp == d.C && d.Kg == row && (total & 7) == 0 && (((uintptr_t)d.w | (uintptr_t)d.fwd) & 15) == 0) {
+    for (int v = tid; v < total / 8; v += nthr) {
+      const float4 a = reinterpret_cast<const float4*>(d.w)[2 * v];
+      const float4 b = reinterpret_cast<const float4*>(d.w)[2 * v + 1];
+      u32x4 o;
+      o.x = pack2(a.x, a.y);
+      o.y = pack2(a.z, a.w);
+      o.z = pack2(b.x, b.y);
+      o.w = pack2(b.z, b.w);
+      reinterpret_cast<u32x4*>(d.fwd)[v] = o;
+    }
+  } else {
+    for (int t = tid; t < total; t += nthr) {
+      const int k = t / d.Kg, col = t - k * d.Kg;
+      const int rs = col / d.Cp, c = col - rs * d.Cp;
       float val = 0.f;
       if (rs < d.RS && c < d.C) val = d.w[((size_t)k * d.RS + rs) * d.C + c];
       d.fwd[t] = f2bf(val);
-    } else {
-      const long long u = t - nf;
-      const int k = (int)(u % d.K);
-      const long long r2 = u / d.K;
-      const int rs = (int)(r2 % d.RS), c = (int)(r2 / d.RS);
-      d.dgrad[u] = f2bf(d.w[((size_t)k * d.RS + rs) * d.C + c]);
+    }
+  }
+}
+
+// dgrad image [C][R*S][K] = transpose of w[K][R*S][C] per tap: 64x64 (k, c) tiles through LDS so
+// that both the fp32 reads (along c) and the bf16 writes (along k) are contiguous.
+__global__ __launch_bounds__(256) void pack_dgrad_batched_kernel(const PackDesc* __restrict__ descs) {
+  __shared__ float tile[64][65];
+  const PackDesc d = descs[blockIdx.y];
+  if (!d.dgrad) return;
+  const int kt = (d.K + 63) / 64, ct = (d.C + 63) / 64;
+  const int ntiles = d.RS * kt * ct;
+  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;  // 64 x 4
+  for (int tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
+    const int rs = tile_id / (kt * ct);
+    const int rem = tile_id - rs * kt * ct;
+    const int k0 = (rem / ct) * 64, c0 = (rem % ct) * 64;
+    __syncthreads();
+    for (int i = ly; i < 64; i += 4) {  // row k0+i, column c0+lx
+      const int k = k0 + i, c = c0 + lx;
+      tile[i][lx] = (k < d.K && c < d.C) ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
+    }
+    __syncthreads();
+    for (int i = ly; i < 64; i += 4) {  // output row c0+i, column k0+lx
+      const int c = c0 + i, k = k0 + lx;
+      if (c < d.C && k < d.K) d.dgrad[((size_t)c * d.RS + rs) * d.K + k] = f2bf(tile[lx][i]);
     }
   }
 }
@@ -186,15 +222,20 @@ extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, 
 }
 
 // descs: device array of n records {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad}
-// (48 bytes each, layout of PackDesc); one launch packs every conv weight of the model.
+// (48 bytes each, layout of PackDesc); two launches pack every conv weight of the model.
 extern "C" size_t avt_pack_desc_bytes(void) { return sizeof(PackDesc); }
 
 extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream) {
   AVT_REQUIRE(descs && n > 0, "pack_conv_weights_batched: bad arguments");
-  long long bx = (max_elems + 255) / 256;
-  if (bx > 512) bx = 512;
+  AVT_REQUIRE(max_elems >= 0 && max_elems < (1ll << 31), "pack_conv_weights_batched: max_elems out of range");
+  long long bx = (max_elems / 8 + 255) / 256;  // fwd: 8 elements per thread
+  if (bx > 256) bx = 256;
   if (bx < 1) bx = 1;
-  hipLaunchKernelGGL(pack_batched_kernel, dim3((unsigned)bx, n), dim3(256), 0, (hipStream_t)stream,
+  long long tx = max_elems / 4096 + 1;  // dgrad: 64x64 tiles
+  if (tx > 512) tx = 512;
+  hipLaunchKernelGGL(pack_fwd_batched_kernel, dim3((unsigned)bx, n), dim3(256), 0, (hipStream_t)stream,
+                     (const PackDesc*)descs);
+  hipLaunchKernelGGL(pack_dgrad_batched_kernel, dim3((unsigned)tx, n), dim3(256), 0, (hipStream_t)stream,
                      (const PackDesc*)descs);
   return check_launch("pack_conv_weights_batched");
 }

@@ -104,31 +104,72 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
-// one block per sample, one thread per channel (C <= 1024)
-__global__ void audio_pool_norm_fwd_kernel(const bf16_t* __restrict__ a, float* __restrict__ an, int* __restrict__ amax,
-                                           float* __restrict__ anorm, int HW, int C) {
+// One block of 512 threads per sample: thread = (8-channel block cg, row group rg); each thread
+// scans rows rg, rg + RG, ... with 16-B loads, then the RG partial (max, first argmax) per channel
+// are merged through LDS (ties -> the smaller row, i.e. the first maximum like torch).
+__global__ __launch_bounds__(512) void audio_pool_norm_fwd_kernel(const bf16_t* __restrict__ a, float* __restrict__ an,
+                                                                  int* __restrict__ amax, float* __restrict__ anorm,
+                                                                  int HW, int C) {
+  __shared__ float sv[512 * 8];
+  __shared__ int si[512 * 8];
   __shared__ float red[16];
-  const int b = blockIdx.x, c = threadIdx.x;
-  float best = -INFINITY;
-  int bi = 0;
-  if (c < C) {
-    const bf16_t* src = a + (size_t)b * HW * C + c;
-    for (int i = 0; i < HW; ++i) {
-      const float f = bf2f(src[(size_t)i * C]);
-      if (f > best || f != f) {
-        best = f;
-        bi = i;
+  const int b = blockIdx.x, cvn = C / 8, RG = 512 / cvn;
+  const int cg = threadIdx.x % cvn, rg = threadIdx.x / cvn;
+  float best[8];
+  int bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    best[e] = -INFINITY;
+    bi[e] = 0;
+  }
+  const bf16_t* src = a + (size_t)b * HW * C + cg * 8;
+  for (int i = rg; i < HW; i += RG) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(src + (size_t)i * C);
+    const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float f = bf2f((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff));
+      if (f > best[e] || (f != f && best[e] == best[e])) {
+        best[e] = f;
+        bi[e] = i;
       }
     }
   }
-  const float ss = block_sum(c < C ? best * best : 0.f, red);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sv[rg * C + cg * 8 + e] = best[e];
+    si[rg * C + cg * 8 + e] = bi[e];
+  }
+  __syncthreads();
+  float m = 0.f;
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    float bv = -INFINITY;
+    int bx = 0;
+    bool first = true;
+    for (int g = 0; g < RG; ++g) {
+      const float v = sv[g * C + c];
+      const int ix = si[g * C + c];
+      if (g >= HW) break;  // row group saw no rows
+      const bool vnan = v != v, bnan = bv != bv;
+      bool take;
+      if (first) take = true;
+      else if (vnan || bnan) take = vnan && (!bnan || ix < bx);
+      else take = v > bv || (v == bv && ix < bx);
+      if (take) {
+        bv = v;
+        bx = ix;
+        first = false;
+      }
+    }
+    m = bv;
+    amax[(size_t)b * C + c] = bx;
+  }
+  const float ss = block_sum(threadIdx.x < C ? m * m : 0.f, red);
   const float nrm = sqrtf(ss);
   const float d = fmaxf(nrm, 1e-12f);
-  if (c < C) {
-    an[(size_t)b * C + c] = best / d;
-    amax[(size_t)b * C + c] = bi;
-  }
-  if (c == 0) anorm[b] = nrm;
+  if (threadIdx.x < C) an[(size_t)b * C + threadIdx.x] = m / d;
+  if (threadIdx.x == 0) anorm[b] = nrm;
 }
 
 // g_pool = (g - an*<an,g>)/max(norm,eps) (identity-free when norm <= eps: g/eps);
@@ -203,9 +244,10 @@ extern "C" int avt_maxpool3s2_bwd(const void* gy, const void* idx, void* gx, int
 extern "C" int avt_audio_pool_norm_fwd(const void* a, float* an, int* amax, float* anorm, int B, int HW, int C,
                                        void* stream) {
   AVT_REQUIRE(a && an && amax && anorm, "audio_pool_norm_fwd: null pointer");
-  AVT_REQUIRE(C % 64 == 0 && C <= 1024, "audio_pool_norm_fwd: C=%d unsupported", C);
-  hipLaunchKernelGGL(audio_pool_norm_fwd_kernel, dim3(B), dim3(C), 0, (hipStream_t)stream, (const bf16_t*)a, an, amax,
-                     anorm, HW, C);
+  AVT_REQUIRE(C >= 64 && C <= 512 && (C & (C - 1)) == 0, "audio_pool_norm_fwd: C=%d unsupported", C);
+  AVT_REQUIRE(HW > 0, "audio_pool_norm_fwd: empty map");
+  hipLaunchKernelGGL(audio_pool_norm_fwd_kernel, dim3(B), dim3(512), 0, (hipStream_t)stream, (const bf16_t*)a, an,
+                     amax, anorm, HW, C);
   return check_launch("audio_pool_norm_fwd");
 }
 

@@ -217,7 +217,7 @@ class AVEngine:
 
     # ----------------------------------------------------------------------------- weights
     def pack_weights(self):
-        """fp32 master weights -> bf16 fwd/dgrad operands of every conv, one launch."""
+        """fp32 master weights -> bf16 fwd/dgrad operands of every conv (two batched launches)."""
         call("avt_pack_conv_weights_batched", P(self._pack_table), self._pack_n, self._pack_max, stream_ptr())
 
     # ----------------------------------------------------------------------------- forward

@@ -198,13 +198,14 @@ class Trunk:
         N, H, W, _ = x.shape
         tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
         c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
-        h0 = torch.empty_like(c0)
-        call("avt_bn_apply", P(c0), P(st0[0]), P(st0[1]), None, None, None, P(h0), N * H1 * W1, 64, 1, stream_ptr())
+        # bn1 -> relu -> maxpool fused: the full-resolution relu(bn1(c0)) is never stored
         H2, W2 = conv_out(H1, 3, 2, 1), conv_out(W1, 3, 2, 1)
         p0 = torch.empty(N, H2, W2, 64, device=x.device, dtype=torch.bfloat16)
         idx = torch.empty(N, H2, W2, 64, device=x.device, dtype=torch.uint8)
-        call("avt_maxpool3s2_fwd", P(h0), P(p0), P(idx), N, H1, W1, 64, stream_ptr())
-        tape.update(c0=c0, st0=st0, h0=h0, idx=idx, H1=H1, W1=W1)
+        carg = torch.empty_like(p0)
+        call("avt_stem_bn_relu_maxpool_fwd", P(c0), P(st0[0]), P(st0[1]), P(p0), P(idx), P(carg), N, H1, W1, 64,
+             stream_ptr())
+        tape.update(c0=c0, st0=st0, idx=idx, carg=carg, H1=H1, W1=W1)
         cur, Hc, Wc = p0, H2, W2
         for blk in self.blocks:
             t = {"x": cur, "H": Hc, "W": Wc}
@@ -239,6 +240,16 @@ class Trunk:
              rows, bn.c, stream_ptr())
         return gc
 
+    def _bn_relu_bwd(self, g, xc, stats, bn: BNSpec, store: Store):
+        """bn -> relu backward with the mask recomputed from (xc, scale, shift) (BasicBlock.bn1)."""
+        rows = xc.numel() // bn.c
+        gc = torch.empty_like(xc)
+        ws = store.stat_acc(bn, "bwd")
+        call("avt_bn_relu_bwd", P(g), P(xc), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]),
+             P(store.param(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".weight")),
+             P(store.grad(bn.prefix + ".bias")), P(gc), P(ws), rows, bn.c, stream_ptr())
+        return gc
+
     def _wgrad(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
         dw = store.grad(spec.name)
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
@@ -268,7 +279,7 @@ class Trunk:
             g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gsum)
             self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
             g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store)
-            g_c1 = self._bn_bwd(g_h1, t["h1"], t["c1"], t["s1"], blk["bn1"], store)
+            g_c1 = self._bn_relu_bwd(g_h1, t["c1"], t["s1"], blk["bn1"], store)
             self._wgrad(t["x"], g_c1, N, Hc, Wc, blk["conv1"], store)
             if identity:
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=gsum)
@@ -280,7 +291,11 @@ class Trunk:
             g = g_x
         # maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)
         H1, W1 = tape["H1"], tape["W1"]
-        g_h0 = torch.empty_like(tape["h0"])
-        call("avt_maxpool3s2_bwd", P(g), P(tape["idx"]), P(g_h0), N, H1, W1, 64, stream_ptr())
-        g_c0 = self._bn_bwd(g_h0, tape["h0"], tape["c0"], tape["st0"], self.bn1, store)
+        c0, st0 = tape["c0"], tape["st0"]
+        g_c0 = torch.empty_like(c0)
+        ws = store.stat_acc(self.bn1, "bwd")
+        call("avt_stem_maxpool_bn_relu_bwd", P(g), P(tape["idx"]), P(tape["carg"]), P(c0), P(st0[0]), P(st0[1]),
+             P(st0[2]), P(st0[3]), P(store.param(self.bn1.prefix + ".weight")),
+             P(store.grad(self.bn1.prefix + ".weight")), P(store.grad(self.bn1.prefix + ".bias")), P(g_c0), P(ws),
+             N, H1, W1, 64, stream_ptr())
         self._wgrad(tape["x"], g_c0, N, tape["H"], tape["W"], self.stem, store)

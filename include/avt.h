@@ -14,6 +14,8 @@
  *   avt_bn_finalize/apply/bwd    nn.BatchNorm2d train mode + nn.ReLU(inplace) + residual add
  *                                (models/base_models.py:39, 46-49, 58-67, 120-121, 141)
  *   avt_maxpool3s2_fwd/bwd       nn.MaxPool2d(3, 2, 1) (models/base_models.py:143, 203)
+ *   avt_stem_*                   stem bn1 -> relu -> maxpool fused fwd/bwd (models/base_models.py:200-203)
+ *   avt_bn_relu_bwd              BasicBlock bn1+relu backward, mask from the pre-activation (base_models.py:47-48)
  *   avt_audio_pool_norm_fwd/bwd  nn.AdaptiveMaxPool2d((1,1)) + F.normalize(dim=1) (model.py:96, 120-122)
  *   avt_hardway_fwd/bwd          AVENet.forward head: normalize, A/A0 einsums, sigmoid trimap,
  *                                sim1/sim/sim2, logits/0.07, weighted_A (model.py:114-154);
@@ -47,10 +49,18 @@ int avt_bn_slots(void);
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
 /* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
- * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages) — an A/B knob */
+ * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
+ * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages) — an A/B knob */
 int avt_set_nt64_config(int cfg);
-/* wgrad split-K policy: about target_blocks blocks in total, at least min_ktiles 32-pixel tiles each */
+/* ... and when the GEMM N is a multiple of 128 (0: 128x128 k32/4 stages (default), 1: 128x128 k64/2,
+ * 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2) */
+int avt_set_nt128_config(int cfg);
+/* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
+ * at least min_ktiles 32-pixel tiles per block */
 int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
+/* wgrad split-K partials go through a slab + reduce up to max_splits splits (fp32 atomics beyond);
+ * wave_cost = per-block fixed cost in k-tiles used by the wave model */
+int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);
@@ -80,6 +90,20 @@ size_t avt_bn_bwd_workspace(long long rows, int C);
 int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
                const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out, void* workspace,
                long long rows, int C, void* stream);
+/* as avt_bn_bwd with g' = g*[fma(xc, scale, shift) > 0] -- the ReLU mask the forward's avt_bn_apply
+ * produced from the same (scale, shift), recomputed instead of read */
+int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale, const float* shift, const float* mean,
+                    const float* invstd, const float* gamma, float* dgamma, float* dbeta, void* gc, void* workspace,
+                    long long rows, int C, void* stream);
+/* stem: y = maxpool3s2(relu(c*scale + shift)) without storing the full-resolution activation; idx = window
+ * argmax (as avt_maxpool3s2_fwd), carg = c at the argmax.  y/idx/carg are [N,P,Q,C] */
+int avt_stem_bn_relu_maxpool_fwd(const void* c, const float* scale, const float* shift, void* y, void* idx,
+                                 void* carg, int N, int H, int W, int C, void* stream);
+/* gc = bn_bwd(relu_bwd(maxpool_bwd(gy))) over the [N,H,W,C] pre-activation c (workspace: avt_bn_bwd_workspace) */
+int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, const void* carg, const void* c, const float* scale,
+                                 const float* shift, const float* mean, const float* invstd, const float* gamma,
+                                 float* dgamma, float* dbeta, void* gc, void* workspace, int N, int H, int W, int C,
+                                 void* stream);
 
 /* ---- pooling ---- */
 int avt_maxpool3s2_fwd(const void* x, void* y, void* idx, int N, int H, int W, int C, void* stream);
@@ -103,7 +127,7 @@ int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, void* stream);
 int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
                          void* stream);
-/* one launch for many convs: descs = device array of n records
+/* two launches (fwd copy, dgrad transpose) for many convs: descs = device array of n records
  * {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad;} (avt_pack_desc_bytes() each) */
 size_t avt_pack_desc_bytes(void);
 int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream);

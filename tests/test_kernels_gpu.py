@@ -132,6 +132,21 @@ def test_conv_variants_bitwise_equal(case):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+    # every tile / k-depth / stage config of the pipelined kernel accumulates in the same k order
+    try:
+        for knob, cfgs in (("avt_set_nt128_config", range(5)), ("avt_set_nt64_config", range(7))):
+            for cfg in cfgs:
+                call(knob, cfg)
+                y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
+                call("avt_conv2d_fwd", P(x), P(wf), P(y), None, N, H, W, C, K, R, R, st, pad, R * R * C, S())
+                dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+                call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), P(x), N, H, W, C, K, R, R, st, pad, S())
+                torch.cuda.synchronize()
+                assert torch.equal(y, outs[0][0]), (knob, cfg)
+                assert torch.equal(dx, outs[0][1]), (knob, cfg)
+    finally:
+        call("avt_set_nt128_config", 0)
+        call("avt_set_nt64_config", 1)
 
 
 @pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
@@ -295,6 +310,110 @@ def test_bn_backward(shape, masked):
     assert rel_err(dbeta, bt.grad) < 1e-3
 
 
+def _bn_batch_stats(c, gamma, beta):
+    """fp32 (scale, shift, mean, invstd) of train-mode BN over NHWC c, as avt_bn_finalize makes them."""
+    C = c.shape[-1]
+    mean = c.double().reshape(-1, C).mean(0)
+    inv = (c.double().reshape(-1, C).var(0, unbiased=False) + 1e-5).rsqrt()
+    scale = (gamma.double() * inv).float()
+    shift = (beta.double() - mean * scale.double()).float()
+    return torch.stack([scale, shift, mean.float(), inv.float()]).to(DEV)
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128)])
+def test_bn_relu_bwd(shape):
+    """BasicBlock.bn1 backward with the ReLU mask recomputed from (c, scale, shift): equals avt_bn_bwd
+    fed the avt_bn_apply output as y, and the fp64 autograd of relu(batch_norm(c))."""
+    N, H, W, C = shape
+    c = (_rand_act(N, H, W, C, 21).float() * 1.3 - 0.2).to(torch.bfloat16)
+    gy = _rand_act(N, H, W, C, 22)
+    g = torch.Generator().manual_seed(23)
+    gamma = 1 + 0.02 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    st = _bn_batch_stats(c, gamma, beta)
+    rows = N * H * W
+    cd, gyd, gmd = c.to(DEV), gy.to(DEV), gamma.to(DEV)
+    y = torch.empty_like(cd)
+    call("avt_bn_apply", P(cd), P(st[0]), P(st[1]), None, None, None, P(y), rows, C, 1, S())
+    outs = []
+    for fused in (True, False):
+        ws = torch.zeros(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
+        dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        gc = torch.empty_like(cd)
+        if fused:
+            call("avt_bn_relu_bwd", P(gyd), P(cd), P(st[0]), P(st[1]), P(st[2]), P(st[3]), P(gmd), P(dgamma),
+                 P(dbeta), P(gc), P(ws), rows, C, S())
+        else:
+            call("avt_bn_bwd", P(gyd), P(y), P(cd), P(st[2]), P(st[3]), P(gmd), P(dgamma), P(dbeta), P(gc), None,
+                 P(ws), rows, C, S())
+        torch.cuda.synchronize()
+        assert not ws[: 16 * C * 2 * 8].any()  # accumulator left zeroed
+        outs.append((gc.float(), dgamma, dbeta))
+    # same mask and sums; only fp64 atomic order may move k1/k2 by an ulp (-> a bf16 ulp of gc)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=8e-3, atol=1e-4)
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+    cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
+    gm = gamma.double().requires_grad_(True)
+    bt = beta.double().requires_grad_(True)
+    F.batch_norm(cn, None, None, gm, bt, True, 0.1, 1e-5).relu().backward(gy.double().permute(0, 3, 1, 2))
+    assert rel_err(outs[0][0], cn.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(outs[0][1], gm.grad) < 1e-2
+    assert rel_err(outs[0][2], bt.grad) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 12, 14, 64), (2, 129, 150, 64), (1, 7, 9, 64), (3, 112, 112, 64)])
+def test_stem_fused(shape):
+    """Stem bn1 -> relu -> maxpool fused both ways (base_models.py:200-203).  fwd: bitwise equal to
+    avt_bn_apply + avt_maxpool3s2_fwd, carg = c at the argmax; bwd: fp64 autograd reference."""
+    N, H, W, C = shape
+    c = (_rand_act(N, H, W, C, 24).float() * 1.5 - 0.3).to(torch.bfloat16)
+    g = torch.Generator().manual_seed(25)
+    gamma = 1 + 0.02 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    st = _bn_batch_stats(c, gamma, beta)
+    cd = c.to(DEV)
+    P2, Q2 = conv_out(H, 3, 2, 1), conv_out(W, 3, 2, 1)
+    y = torch.empty(N, P2, Q2, C, device=DEV, dtype=torch.bfloat16)
+    idx = torch.empty(N, P2, Q2, C, device=DEV, dtype=torch.uint8)
+    carg = torch.empty_like(y)
+    call("avt_stem_bn_relu_maxpool_fwd", P(cd), P(st[0]), P(st[1]), P(y), P(idx), P(carg), N, H, W, C, S())
+    h = torch.empty_like(cd)
+    call("avt_bn_apply", P(cd), P(st[0]), P(st[1]), None, None, None, P(h), N * H * W, C, 1, S())
+    y2, idx2 = torch.empty_like(y), torch.empty_like(idx)
+    call("avt_maxpool3s2_fwd", P(h), P(y2), P(idx2), N, H, W, C, S())
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2) and torch.equal(idx, idx2)
+    # carg == c at (2p-1+idx//3, 2q-1+idx%3)
+    ii = idx.long().cpu()
+    hh = (2 * torch.arange(P2).view(1, P2, 1, 1) - 1 + ii // 3).clamp(0, H - 1)
+    ww = (2 * torch.arange(Q2).view(1, 1, Q2, 1) - 1 + ii % 3).clamp(0, W - 1)
+    nn_ = torch.arange(N).view(N, 1, 1, 1).expand_as(ii)
+    cc = torch.arange(C).view(1, 1, 1, C).expand_as(ii)
+    assert torch.equal(carg.cpu(), c[nn_, hh, ww, cc])
+
+    gy = _rand_act(N, P2, Q2, C, 26)
+    ws = torch.zeros(int(query("avt_bn_bwd_workspace", N * H * W, C)), device=DEV, dtype=torch.uint8)
+    dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    gc = torch.empty_like(cd)
+    call("avt_stem_maxpool_bn_relu_bwd", P(gy.to(DEV)), P(idx), P(carg), P(cd), P(st[0]), P(st[1]), P(st[2]),
+         P(st[3]), P(gamma.to(DEV)), P(dgamma), P(dbeta), P(gc), P(ws), N, H, W, C, S())
+    torch.cuda.synchronize()
+    assert not ws[: 16 * C * 2 * 8].any()
+    cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
+    gm = gamma.double().requires_grad_(True)
+    bt = beta.double().requires_grad_(True)
+    hr = F.batch_norm(cn, None, None, gm, bt, True, 0.1, 1e-5).relu()
+    # route the pool through the kernel's bf16 activation values (straight-through), so bf16 ties
+    # pick the same (first) window position; the gradient itself stays fp64
+    hk = h.cpu().double().permute(0, 3, 1, 2)
+    hr = hr + (hk - hr).detach()
+    F.max_pool2d(hr, 3, 2, 1).backward(gy.double().permute(0, 3, 1, 2))
+    assert rel_err(gc, cn.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(dgamma, gm.grad) < 1e-2
+    assert rel_err(dbeta, bt.grad) < 1e-3
+
+
 # ------------------------------------------------------------------------------------------ pools
 @pytest.mark.parametrize("shape", [(2, 12, 14, 64), (2, 129, 150, 64), (1, 7, 9, 64)])
 def test_maxpool(shape):
@@ -391,6 +510,37 @@ def test_hardway_head(B, h, w, trimap, neg):
     assert (wA.cpu().double() - rwA.detach().reshape(B, Pn)).abs().max() < 1e-5
     assert rel_err(gan, at.grad) < 2e-3
     assert rel_err(gv, vt.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_pack_batched_matches_single():
+    """avt_pack_conv_weights_batched (vector fwd copy + LDS-tiled dgrad transpose) == the per-conv
+    pack, bitwise, incl. the padded stem layout, a misaligned source and partial 64x64 tiles."""
+    import struct
+    # K, R, C, Cp, Kg, flat offset (floats)
+    cases = [(64, 7, 3, 4, 224, 0), (64, 7, 1, 1, 64, 9408), (128, 3, 64, 64, 576, 12544),
+             (96, 3, 40, 40, 360, 86272), (256, 1, 128, 128, 128, 120833), (512, 3, 512, 512, 4608, 153604)]
+    total = max(o + K * R * R * C for K, R, C, _, _, o in cases)
+    g = torch.Generator().manual_seed(40)
+    flat = torch.randn(total, generator=g).to(DEV)
+    descs, singles, outs, maxel = [], [], [], 0
+    for K, R, C, Cp, Kg, o in cases:
+        w = flat[o:o + K * R * R * C]
+        wf = torch.empty(K, Kg, device=DEV, dtype=torch.bfloat16)
+        wt = torch.empty(C, R * R * K, device=DEV, dtype=torch.bfloat16) if C == Cp else None
+        descs.append(struct.pack("<QQQiiiiii", w.data_ptr(), wf.data_ptr(), 0 if wt is None else wt.data_ptr(),
+                                 K, R * R, C, Cp, Kg, 0))
+        maxel = max(maxel, K * Kg + (0 if wt is None else wt.numel()))
+        outs.append((wf, wt))
+        sf, st_ = torch.empty_like(wf), (torch.empty_like(wt) if wt is not None else None)
+        call("avt_pack_conv_weight", P(w), K, R, R, C, Cp, Kg, P(sf), P(st_), S())
+        singles.append((sf, st_))
+    table = torch.frombuffer(bytearray(b"".join(descs)), dtype=torch.uint8).to(DEV)
+    call("avt_pack_conv_weights_batched", P(table), len(descs), maxel, S())
+    torch.cuda.synchronize()
+    for (wf, wt), (sf, st_) in zip(outs, singles):
+        assert torch.equal(wf, sf)
+        if wt is not None:
+            assert torch.equal(wt, st_)
 
 
 def test_adam_matches_torch():

@@ -53,12 +53,15 @@ def main():
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--only", default="")
-    ap.add_argument("--wgrad-policy", default="1024,8")
+    ap.add_argument("--wgrad-policy", default="0,4", help="';'-separated target_blocks,min_kt (0 = wave model)")
+    ap.add_argument("--slab-max", default="32,16", help="avt_set_wgrad_slab_max(max_splits, wave_cost)")
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
+    ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
+    call("avt_set_wgrad_slab_max", *(int(v) for v in args.slab_max.split(",")))
     kinds = args.kinds.split(",")
     tot = {}
     for name, H, W, C, K, R, st, pad in SHAPES:
@@ -91,6 +94,19 @@ def main():
                                              pad, S()))
                     line += f" nt64[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
             call("avt_set_nt64_config", 1)
+        if args.nt128 and K % 128 == 0 or args.nt128 and C % 128 == 0:
+            for cfg in [int(s) for s in args.nt128.split(",")]:
+                call("avt_set_nt128_config", cfg)
+                call("avt_set_conv_variant", 1)
+                if K % 128 == 0:
+                    ms = timeit(lambda: call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st,
+                                             pad, kg, S()))
+                    line += f" | nt128[{cfg}] fwd {flops / ms / 1e9:6.0f}"
+                if C % 128 == 0:
+                    ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
+                                             pad, S()))
+                    line += f" nt128[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
+            call("avt_set_nt128_config", 0)
         for v in [int(s) for s in args.variants.split(",")]:
             call("avt_set_conv_variant", v)
             if "fwd" in kinds:
@@ -113,7 +129,7 @@ def main():
                                              P(ws), wsb if args.slab else 0, S()))
                     line += f" wgrad[{tb},{mk}] {flops / ms / 1e9:6.0f}"
                     tot[("wgrad" + pol, v)] = tot.get(("wgrad" + pol, v), 0) + ms
-                call("avt_set_wgrad_policy", 1024, 8)
+                call("avt_set_wgrad_policy", 0, 4)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
