@@ -32,6 +32,7 @@ SIGNATURES = {
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_nt128_config": (_I, [_I]),
     "avt_set_wgrad_slab_max": (_I, [_I, _I]),
+    "avt_set_wgrad_tiles": (_I, [_I]),
     "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
@@ -68,7 +69,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     """Compile csrc/*.hip for gfx950 into libavt.so (in-tree)."""
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     if not force and os.path.exists(LIB_PATH):
-        newest = max(os.path.getmtime(s) for s in srcs + [os.path.join(CSRC, "avt_common.h")])
+        deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+        newest = max(os.path.getmtime(s) for s in deps)
         if os.path.getmtime(LIB_PATH) >= newest:
             return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

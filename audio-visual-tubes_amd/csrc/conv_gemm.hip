@@ -458,11 +458,12 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_tn_pipe.h"
 
 static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
-static int g_nt128_config = 0;  // ... and for GEMM N % 128 == 0
+static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
 static int g_wgrad_blocks = 0;     // wgrad split-K: 0 = wave model (wgrad_plan), >0 = fixed block target
 static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
+static int g_wgrad_big = 1;        // allow the 8-wave 256-wide wgrad tiles
 static int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -493,13 +494,13 @@ extern "C" int avt_set_conv_variant(int v) {
 }
 
 extern "C" int avt_set_nt64_config(int cfg) {
-  AVT_REQUIRE(cfg >= 0 && cfg <= 6, "set_nt64_config: cfg in 0..6");
+  AVT_REQUIRE(cfg >= 0 && cfg <= 8, "set_nt64_config: cfg in 0..8");
   g_nt64_config = cfg;
   return AVT_OK;
 }
 
 extern "C" int avt_set_nt128_config(int cfg) {
-  AVT_REQUIRE(cfg >= 0 && cfg <= 4, "set_nt128_config: cfg=%d out of range", cfg);
+  AVT_REQUIRE(cfg >= -1 && cfg <= 6, "set_nt128_config: cfg=%d out of range", cfg);
   avt::g_nt128_config = cfg;
   return AVT_OK;
 }
@@ -518,6 +519,11 @@ extern "C" int avt_set_wgrad_slab_max(int max_splits, int wave_cost) {
   return AVT_OK;
 }
 
+extern "C" int avt_set_wgrad_tiles(int big) {
+  avt::g_wgrad_big = big ? 1 : 0;
+  return AVT_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------------------
@@ -528,7 +534,8 @@ static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgs& ta, hipStre
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
   if (grid > 0)
-    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK>), dim3(grid), dim3(256), 0, st, p, ta);
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK>), dim3(grid), dim3(WM * WN * 64), 0, st, p,
+                       ta);
 }
 
 // Builds the tap list(s) and launches: fwd / stride-1 dgrad in one launch; a stride-2 dgrad as
@@ -536,7 +543,7 @@ static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgs& ta, hipStre
 template <int MODE, int WM, int WN, int TM, int TN, int NST = 4, int BK = 32>
 static void launch_glds(const GemmNTParams& p, hipStream_t st) {
   if (BK == 64 && p.IC % 64 != 0) {  // a 64-deep k-tile needs whole 64-channel taps
-    launch_glds<MODE, WM, WN, TM, TN, (NST > 3 ? NST : 3), 32>(p, st);
+    launch_glds<MODE, 2, 2, 2, (WN * TN * 32) / 64, 3, 32>(p, st);  // 4-wave k32 tile of the same width
     return;
   }
   NTPipeArgs ta{};
@@ -586,11 +593,16 @@ template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
   if (CVEC == 8 && conv_variant() == 1) {
     if (p.Ng % 128 == 0) {
-      switch (g_nt128_config) {
+      // default: 256-row tiles (8 waves) where the GEMM is tall enough to fill the chip with them
+      // (layer2, the stride-2 convs), 128 x 128 k64 tiles for the short layer3/4 GEMMs
+      const int cfg = g_nt128_config >= 0 ? g_nt128_config : (p.M >= 65536 ? 6 : 1);
+      switch (cfg) {
         case 1: launch_glds<MODE, 2, 2, 2, 2, 2, 64>(p, st); break;  // 128 x 128, k64, 2 stages
         case 2: launch_glds<MODE, 2, 2, 2, 2, 3, 64>(p, st); break;  // 128 x 128, k64, 3 stages
         case 3: launch_glds<MODE, 2, 2, 4, 2, 3>(p, st); break;      // 256 x 128, k32, 3 stages
         case 4: launch_glds<MODE, 2, 2, 4, 2, 2, 64>(p, st); break;  // 256 x 128, k64, 2 stages
+        case 5: launch_glds<MODE, 4, 2, 2, 2, 2, 64>(p, st); break;  // 256 x 128, 8 waves, k64, 2 stages
+        case 6: launch_glds<MODE, 4, 2, 2, 2, 3>(p, st); break;      // 256 x 128, 8 waves, k32, 3 stages
         default: launch_glds<MODE, 2, 2, 2, 2>(p, st); break;        // 128 x 128, k32, 4 stages
       }
     } else {  // 64-wide N (layer1 / stem-fed convs)
@@ -601,6 +613,8 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
         case 4: launch_glds<MODE, 2, 2, 2, 1, 3, 64>(p, st); break;  // 128 x 64, k64, 3 stages
         case 5: launch_glds<MODE, 4, 1, 2, 2, 2, 64>(p, st); break;  // 256 x 64, k64, 2 stages
         case 6: launch_glds<MODE, 2, 2, 2, 1, 2, 64>(p, st); break;  // 128 x 64, k64, 2 stages
+        case 7: launch_glds<MODE, 4, 2, 2, 1, 3, 64>(p, st); break;  // 256 x 64, 8 waves, k64, 3 stages
+        case 8: launch_glds<MODE, 4, 2, 2, 1, 2, 64>(p, st); break;  // 256 x 64, 8 waves, k64, 2 stages
         default: launch_glds<MODE, 2, 2, 2, 1, 3>(p, st); break;  // 128 x 64, 3 stages
       }
     }
@@ -692,20 +706,31 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
   p.Kred = N * p.P * p.Q;
   const int ncols = R * S * Cp;
+  pl.pipe = (Cp % 8 == 0) && conv_variant() == 1;
   pl.BN = (ncols % 128 == 0 || ncols > 128) ? 128 : 64;
   pl.BM = (K % 128 == 0 && Cp % 8 == 0) || (K % 128 == 0 && Cp == 4) ? 128 : 64;
+  // 8-wave 256-wide tiles halve the LDS fill bytes per flop where the GEMM is wide enough
+  // (layer4: K_out 512, R*S*C >= 2304); split-K supplies the parallelism
+  if (pl.pipe && g_wgrad_big) {
+    if (K % 256 == 0 && K >= 512 && pl.BN == 128) pl.BM = 256;  // measured: a loss on layer3 (K_out 256)
+    if (ncols >= 2048 && pl.BM == 256) pl.BN = 256;
+  }
   p.Ng = ((ncols + pl.BN - 1) / pl.BN) * pl.BN;
   pl.tiles = (p.Mg / pl.BM) * (p.Ng / pl.BN);
   const int nkt = (p.Kred + 31) / 32;
   // Split-K count.  The grid runs in "waves" of resident blocks (CUs x blocks per CU, set by the
-  // NST=4 ring's LDS: 256*(BM+BN) bytes per block).  For w = 1..4 waves take the largest split
-  // count that fits, s_w = floor(w*slots/tiles), and keep the one with the least
-  // w * (ceil(nkt/s_w) + wave_cost) -- k-tiles per block plus its fixed prologue/epilogue cost.
+  // ring's LDS: 4 stages x 32 pixels x (BM+BN) bf16 for the 4-wave tiles, 3 stages for the 8-wave
+  // ones, whose 256x256 form is also held to one block per CU by its registers).  For w = 1..4
+  // waves take the largest split count that fits, s_w = floor(w*slots/tiles), and keep the one
+  // with the least w * (ceil(nkt/s_w) + wave_cost) -- k-tiles per block plus its fixed
+  // prologue/epilogue cost.
   int splits;
   if (g_wgrad_blocks > 0) {
     splits = g_wgrad_blocks / pl.tiles;
   } else {
-    const int occ = max(1, 163840 / (256 * (pl.BM + pl.BN)));
+    const bool big = pl.BM == 256 || pl.BN == 256;
+    int occ = max(1, 163840 / ((big ? 192 : 256) * (pl.BM + pl.BN)));
+    if (pl.BM == 256 && pl.BN == 256) occ = 1;
     const long long slots = (long long)num_cus() * occ;
     long long best = -1;
     splits = 1;
@@ -726,7 +751,6 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;
   pl.splits = (nkt + kps - 1) / kps;
   p.kt_per_split = kps;
-  pl.pipe = (Cp % 8 == 0) && conv_variant() == 1;
   // slab + reduce pass for moderate split counts (measured faster on layer3/4); very deep splits
   // (layer1/2: 100-200 splits of a small output) keep the fp32 atomics, which overlap the compute
   pl.slab_bytes = (pl.pipe && pl.splits > 1 && pl.splits <= g_wgrad_slab_max)
@@ -746,11 +770,17 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
     pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
     pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
     pp.slab = slab;
-    constexpr int TM = BM / 64, TN = BN / 64;
-    hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, TM, TN, 4>), dim3(pl.tiles * pl.splits), dim3(256), 0, st, pp);
+    if constexpr (BM == 256 && BN == 256)
+      hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 3>), dim3(pl.tiles * pl.splits), dim3(512), 0, st, pp);
+    else if constexpr (BM == 256)
+      hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 2, 3>), dim3(pl.tiles * pl.splits), dim3(512), 0, st, pp);
+    else
+      hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 4>), dim3(pl.tiles * pl.splits), dim3(256), 0, st,
+                         pp);
     return;
   }
-  hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(pl.tiles, pl.splits), dim3(256), 0, st, p);
+  if constexpr (BM <= 128)
+    hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(pl.tiles, pl.splits), dim3(256), 0, st, p);
 }
 
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, long long n,
@@ -796,6 +826,9 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
     if (BM == 128) launch_tn<4, 128, 128>(pl, slab, st); else launch_tn<4, 64, 128>(pl, slab, st);
   } else if (Cp == 1) {
     if (BN == 128) launch_tn<1, 64, 128>(pl, slab, st); else launch_tn<1, 64, 64>(pl, slab, st);
+  } else if (BM == 256) {
+    if (BN == 256) launch_tn<8, 256, 256>(pl, slab, st);
+    else launch_tn<8, 256, 128>(pl, slab, st);  // the plan pairs BM 256 with BN >= 128 only
   } else if (BN == 128) {
     if (BM == 128) launch_tn<8, 128, 128>(pl, slab, st); else launch_tn<8, 64, 128>(pl, slab, st);
   } else {

@@ -49,17 +49,19 @@ __device__ __forceinline__ int swz_rb(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-// 4 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32; BK = k-tile
+// 4 or 8 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32; BK = k-tile
 // depth (32 or 64 bf16: 64-B or whole 128-B lines per gathered row and tap).
 template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32>
-__global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPipeArgs ta) {
-  static_assert(WM * WN == 4, "4 waves");
+__global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams p, NTPipeArgs ta) {
+  constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BK == 32 || BK == 64, "BK");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int RB = BK * 2;                 // bytes per LDS row
   constexpr int CPR = RB / 16;               // 16-B chunks per row
   constexpr int RPI = 1024 / RB;             // rows per 1 KiB buffer-lds instruction
-  constexpr int AR = BM / (4 * RPI), BR = BN / (4 * RPI);  // instructions per wave per tile
+  constexpr int AR = BM / (NW * RPI), BR = BN / (NW * RPI);  // instructions per wave per tile
+  static_assert(AR >= 1 && BR >= 1 && AR * NW * RPI == BM && BR * NW * RPI == BN, "tile/wave split");
   constexpr int LPT = AR + BR;
   constexpr int STAGE = (BM + BN) * RB;
   constexpr int CT_LD = BN + 8;
@@ -119,6 +121,15 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
   const int cpt = p.IC / BK;  // k-tiles per tap
   const int nkt = ta.ntaps * cpt;
 
+  // Tap table in VGPRs: lane t (< ntaps) holds tap t's activation and weight byte offsets; the
+  // k loop reads them with v_readlane (no scalar-memory load, hence no lgkmcnt wait that would
+  // also drain the LDS fragment reads, on the loop's critical path).
+  int lane_tapoff = 0, lane_tapw = 0;
+  if (lane < ta.ntaps) {
+    lane_tapoff = (ta.tap_dy[lane] * p.IW + ta.tap_dx[lane]) * p.IC * 2;
+    lane_tapw = ta.tap_w[lane] * p.IC * 2;
+  }
+
   // incremental state of the next tile to issue (wave-uniform)
   int it_t = 0, it_c = 0, it_k = 0;
   auto issue = [&](int stage) {
@@ -126,8 +137,8 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
     char* Bs = As + BM * RB;
     const bool live = it_k < nkt;
     const int t = live ? it_t : 0;
-    const int tapoff = ((ta.tap_dy[t] * p.IW + ta.tap_dx[t]) * p.IC + it_c) * 2;
-    const unsigned boff = (unsigned)((ta.tap_w[t] * p.IC + it_c) * 2);  // weight k offset (Kg = R*S*IC)
+    const int tapoff = __builtin_amdgcn_readlane(lane_tapoff, t) + it_c * 2;
+    const unsigned boff = (unsigned)(__builtin_amdgcn_readlane(lane_tapw, t) + it_c * 2);  // Kg = R*S*IC
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const unsigned voff = a_off0[i] + (unsigned)tapoff;
@@ -156,29 +167,40 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
   for (int t = 0; t < NST - 1; ++t) issue(t);
 
   const int frow = lane & 31, fhalf = lane >> 5;
+  constexpr int KS = BK / 16;
+  bf16x8 af[2][TM], bfr[2][TN];  // fragments of k-step ks live in [ks & 1]
+  auto load_frags = [&](const char* As, const char* Bs, int ks, int buf) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * (BM / WM) + i * 32 + frow;
+      af[buf][i] = *reinterpret_cast<const bf16x8*>(As + swz_rb<RB>(row, ks * 2 + fhalf));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * (BN / WN) + j * 32 + frow;
+      bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + swz_rb<RB>(row, ks * 2 + fhalf));
+    }
+  };
   for (int kt = 0; kt < nkt; ++kt) {
     wait_vmcnt<(NST - 2) * LPT>();  // tile kt has landed (NST-2 younger tiles may be in flight)
     __builtin_amdgcn_s_barrier();
-    issue((kt + NST - 1) % NST);  // the stage read in iteration kt-1; every wave has passed that
     const char* As = smem + (kt % NST) * STAGE;
     const char* Bs = As + BM * RB;
+    load_frags(As, Bs, 0, 0);
+    issue((kt + NST - 1) % NST);  // the stage read in iteration kt-1; every wave has passed that
+    // k-steps software-pipelined: the fragments of step ks+1 are read while step ks multiplies
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * (BM / WM) + i * 32 + frow;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + swz_rb<RB>(row, ks * 2 + fhalf));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / WN) + j * 32 + frow;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + swz_rb<RB>(row, ks * 2 + fhalf));
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+        load_frags(As, Bs, ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);  // the next step's reads stay ahead of this step's MFMAs
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+      if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
     }
   }
   wait_vmcnt<0>();  // drain the dummy tail loads before the ring is reused
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
     }
     __syncthreads();
     double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
-    for (int c = tid; c < BN; c += 256) {
+    for (int c = tid; c < BN; c += NT) {
       double s = 0.0, m2 = 0.0;
 #pragma unroll
       for (int k = 0; k < WM; ++k) {
@@ -248,7 +270,7 @@ __global__ __launch_bounds__(256) void conv_nt_pipe_kernel(GemmNTParams p, NTPip
       }
   __syncthreads();
   constexpr int OCPR = BN / 8;
-  for (int idx = tid; idx < BM * OCPR; idx += 256) {
+  for (int idx = tid; idx < BM * OCPR; idx += NT) {
     const int r = idx / OCPR, cc = idx - r * OCPR;
     if (r >= rows_valid) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);

@@ -38,18 +38,21 @@ struct GemmTNPipeParams {
 
 template <int ROWB>
 __device__ __forceinline__ int tn_swz(int row) {  // chunk XOR for a row of ROWB bytes
-  return ROWB == 256 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
+  return ROWB >= 256 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
 }
 
+// 4 or 8 waves as WM x WN, each wave TM x TN tiles of 32x32 (8 waves need BM, BN >= 128)
 template <int WM, int WN, int TM, int TN, int NST>
-__global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
-  static_assert(WM * WN == 4, "4 waves");
+__global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
+  constexpr int NW = WM * WN;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  static_assert(BM == 64 || BM == 128, "BM");
-  static_assert(BN == 64 || BN == 128, "BN");
+  static_assert(BM == 64 || BM == 128 || BM == 256, "BM");
+  static_assert(BN == 64 || BN == 128 || BN == 256, "BN");
   constexpr int AROWB = BM * 2, BROWB = BN * 2;          // bytes per pixel row
   constexpr int A_RPI = 1024 / AROWB, B_RPI = 1024 / BROWB;  // rows per 1 KiB instruction
-  constexpr int AI = 32 / A_RPI / 4, BI = 32 / B_RPI / 4;    // instructions per wave per tile
+  constexpr int AI = 32 / A_RPI / NW, BI = 32 / B_RPI / NW;  // instructions per wave per tile
+  static_assert(AI >= 1 && BI >= 1 && AI * A_RPI * NW == 32 && BI * B_RPI * NW == 32, "tile/wave split");
   constexpr int LPT = AI + BI;
   constexpr int A_BYTES = 32 * AROWB, STAGE = 32 * (AROWB + BROWB);
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
@@ -75,18 +78,11 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)pp.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)pp.x_bytes, 0x00020000);
 
-  // A (dy) lanes: row-in-instruction and logical chunk (fixed per lane)
+  // Lanes: row-in-instruction and physical chunk; the logical chunk a lane fetches is its
+  // physical chunk XOR the swizzle of the LDS row it fills (per instruction: 512-B rows put only
+  // two rows in one 1 KiB instruction, so the row's swizzle depends on the instruction).
   const int a_r = lane / (AROWB / 16), a_pc = lane % (AROWB / 16);
-  const int a_lc = a_pc ^ tn_swz<AROWB>(a_r);
-  const unsigned a_coff = (unsigned)((m0 + a_lc * 8) * 2);
-  // B (x gather) lanes
   const int b_r = lane / (BROWB / 16), b_pc = lane % (BROWB / 16);
-  const int b_lc = b_pc ^ tn_swz<BROWB>(b_r);
-  const int col = n0 + b_lc * 8;
-  const int rs = col / p.Cp;
-  const int b_c = col - rs * p.Cp;
-  const int b_rr = rs / p.S, b_ss = rs - b_rr * p.S;
-  const bool b_colok = col < p.R * p.S * p.Cp;
 
   // Per-slot pixel state, advanced incrementally by 32 pixels per tile (no divisions in the loop):
   // 32 = step_oh*Q + step_ow; offsets use 24-bit multiplies (full-rate v_mul_u32_u24).
@@ -94,13 +90,20 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
   const unsigned rowB = (unsigned)(p.W * p.Cp * 2), pixB = (unsigned)(p.Cp * 2);
   const unsigned imgB = (unsigned)(p.H * p.W * p.Cp * 2);
   const int step_oh = 32 / p.Q, step_ow = 32 - (32 / p.Q) * p.Q;
-  const int y_off = b_rr - p.pad, x_off = b_ss - p.pad;
-  const unsigned cB = (unsigned)(b_c * 2);
-  int b_pix[BI], b_oh[BI], b_ow[BI];
-  unsigned b_nb[BI];
+  int b_pix[BI], b_oh[BI], b_ow[BI], y_off[BI], x_off[BI];
+  unsigned b_nb[BI], cB[BI];
+  bool b_colok[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
     const int row = (wid * BI + i) * B_RPI + b_r;
+    const int col = n0 + (b_pc ^ tn_swz<BROWB>(row)) * 8;  // (r, s, c) patch column of this lane
+    const int rs = col / p.Cp;
+    const int b_c = col - rs * p.Cp;
+    const int b_rr = rs / p.S, b_ss = rs - b_rr * p.S;
+    b_colok[i] = col < p.R * p.S * p.Cp;
+    y_off[i] = b_rr - p.pad;
+    x_off[i] = b_ss - p.pad;
+    cB[i] = (unsigned)(b_c * 2);
     const int pix = kt_begin * 32 + row;
     const unsigned n = magic_div((unsigned)pix, pp.div_pq);
     const unsigned rem = (unsigned)pix - n * (unsigned)(p.P * p.Q);
@@ -115,6 +118,7 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int row = (wid * AI + i) * A_RPI + a_r;
+    const unsigned a_coff = (unsigned)((m0 + (a_pc ^ tn_swz<AROWB>(row)) * 8) * 2);
     a_pix[i] = kt_begin * 32 + row;
     a_off[i] = (unsigned)a_pix[i] * (unsigned)(p.Mg * 2) + a_coff;
   }
@@ -133,9 +137,10 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
-      const int y = (b_oh[i] << sh) + y_off, x = (b_ow[i] << sh) + x_off;
-      const bool ok = live && b_colok && b_pix[i] < p.Kred && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
-      const unsigned off = b_nb[i] + __umul24((unsigned)y, rowB) + __umul24((unsigned)x, pixB) + cB;
+      const int y = (b_oh[i] << sh) + y_off[i], x = (b_ow[i] << sh) + x_off[i];
+      const bool ok =
+          live && b_colok[i] && b_pix[i] < p.Kred && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const unsigned off = b_nb[i] + __umul24((unsigned)y, rowB) + __umul24((unsigned)x, pixB) + cB[i];
       const unsigned m = 0u - (unsigned)ok;  // branch-free select
       buf_lds16(rsb, Bs + (wid * BI + i) * 1024, (off & m) | (kOOB & ~m));
       b_pix[i] += 32;
@@ -170,40 +175,48 @@ __global__ __launch_bounds__(256) void conv_tn_pipe_kernel(GemmTNPipeParams pp) 
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) issue(kt_begin + s, s);
 
+  bf16x8 af[2][TM], bfr[2][TN];  // fragments of k-step ks live in [ks & 1]
+  auto load_frags = [&](const char* As, const char* Bs, int ks, int buf) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int c = wm * (BM / WM) + i * 32 + tr_col;
+      const int off = ((c >> 3) ^ a_sw) * 16 + (c & 7) * 2;
+      const char* a0 = As + (ks * 16 + tr_row) * AROWB + off;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * AROWB));
+      short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      af[buf][i] = __builtin_bit_cast(bf16x8, tmp);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int c = wn * (BN / WN) + j * 32 + tr_col;
+      const int off = ((c >> 3) ^ b_sw) * 16 + (c & 7) * 2;
+      const char* b0 = Bs + (ks * 16 + tr_row) * BROWB + off;
+      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * BROWB));
+      short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bfr[buf][j] = __builtin_bit_cast(bf16x8, tmp);
+    }
+  };
   for (int k = 0; k < nkt; ++k) {
     wait_vmcnt<(NST - 2) * LPT>();
     __builtin_amdgcn_s_barrier();
-    issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);
     const char* As = smem + (k % NST) * STAGE;
     const char* Bs = As + A_BYTES;
+    load_frags(As, Bs, 0, 0);
+    issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);
+    // step 1's fragments are read while step 0 multiplies
+    load_frags(As, Bs, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[TM], bfr[TN];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int c = wm * (BM / WM) + i * 32 + tr_col;
-        const int off = ((c >> 3) ^ a_sw) * 16 + (c & 7) * 2;
-        const char* a0 = As + (ks * 16 + tr_row) * AROWB + off;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * AROWB));
-        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, tmp);
-      }
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn * (BN / WN) + j * 32 + tr_col;
-        const int off = ((c >> 3) ^ b_sw) * 16 + (c & 7) * 2;
-        const char* b0 = Bs + (ks * 16 + tr_row) * BROWB + off;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0 + 4 * BROWB));
-        short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, tmp);
-      }
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
   }
   wait_vmcnt<0>();
 

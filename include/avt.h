@@ -50,10 +50,12 @@ int avt_bn_slots(void);
 int avt_set_conv_variant(int variant);
 /* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
  * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
- * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages) — an A/B knob */
+ * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
+ * — an A/B knob */
 int avt_set_nt64_config(int cfg);
-/* ... and when the GEMM N is a multiple of 128 (0: 128x128 k32/4 stages (default), 1: 128x128 k64/2,
- * 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2) */
+/* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
+ * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
+ * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */
 int avt_set_nt128_config(int cfg);
 /* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
  * at least min_ktiles 32-pixel tiles per block */
@@ -61,6 +63,8 @@ int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 /* wgrad split-K partials go through a slab + reduce up to max_splits splits (fp32 atomics beyond);
  * wave_cost = per-block fixed cost in k-tiles used by the wave model */
 int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
+/* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
+int avt_set_wgrad_tiles(int big);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);

@@ -134,7 +134,7 @@ def test_conv_variants_bitwise_equal(case):
     assert torch.equal(outs[0][1], outs[1][1])
     # every tile / k-depth / stage config of the pipelined kernel accumulates in the same k order
     try:
-        for knob, cfgs in (("avt_set_nt128_config", range(5)), ("avt_set_nt64_config", range(7))):
+        for knob, cfgs in (("avt_set_nt128_config", range(7)), ("avt_set_nt64_config", range(9))):
             for cfg in cfgs:
                 call(knob, cfg)
                 y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
@@ -145,7 +145,7 @@ def test_conv_variants_bitwise_equal(case):
                 assert torch.equal(y, outs[0][0]), (knob, cfg)
                 assert torch.equal(dx, outs[0][1]), (knob, cfg)
     finally:
-        call("avt_set_nt128_config", 0)
+        call("avt_set_nt128_config", -1)
         call("avt_set_nt64_config", 1)
 
 
@@ -206,15 +206,20 @@ def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
          S())
 
 
+@pytest.mark.parametrize("big", [1, 0])
 @pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wgrad(case, slab):
+def test_conv_wgrad(case, slab, big):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
     dy = _rand_act(N, Pq, Qq, K, 9)
     dw = torch.full((K, R, R, C), 0.25, device=DEV)  # accumulates into an existing gradient
-    wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
+    try:
+        call("avt_set_wgrad_tiles", big)
+        wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
+    finally:
+        call("avt_set_wgrad_tiles", 1)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()

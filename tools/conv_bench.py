@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--wgrad-policy", default="0,4", help="';'-separated target_blocks,min_kt (0 = wave model)")
     ap.add_argument("--slab-max", default="32,16", help="avt_set_wgrad_slab_max(max_splits, wave_cost)")
+    ap.add_argument("--wgrad-tiles", default="1", help="comma list of avt_set_wgrad_tiles values to sweep")
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
@@ -106,7 +107,7 @@ def main():
                     ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
                                              pad, S()))
                     line += f" nt128[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
-            call("avt_set_nt128_config", 0)
+            call("avt_set_nt128_config", -1)
         for v in [int(s) for s in args.variants.split(",")]:
             call("avt_set_conv_variant", v)
             if "fwd" in kinds:
@@ -120,16 +121,20 @@ def main():
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
                 tot[("dgrad", v)] = tot.get(("dgrad", v), 0) + ms
             if "wgrad" in kinds and v == 1:
-                for pol in args.wgrad_policy.split(";"):
-                    tb, mk = (int(s) for s in pol.split(","))
-                    call("avt_set_wgrad_policy", tb, mk)
-                    wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
-                    ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
-                    ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st, pad,
-                                             P(ws), wsb if args.slab else 0, S()))
-                    line += f" wgrad[{tb},{mk}] {flops / ms / 1e9:6.0f}"
-                    tot[("wgrad" + pol, v)] = tot.get(("wgrad" + pol, v), 0) + ms
+                for big in [int(t) for t in args.wgrad_tiles.split(",")]:
+                    call("avt_set_wgrad_tiles", big)
+                    for pol in args.wgrad_policy.split(";"):
+                        tb, mk = (int(s) for s in pol.split(","))
+                        call("avt_set_wgrad_policy", tb, mk)
+                        wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+                        ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
+                        ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st,
+                                                 pad, P(ws), wsb if args.slab else 0, S()))
+                        line += f" wgrad[t{big},{tb},{mk}] {flops / ms / 1e9:6.0f}"
+                        key = f"wgrad_t{big}_{pol}"
+                        tot[(key, v)] = tot.get((key, v), 0) + ms
                 call("avt_set_wgrad_policy", 0, 4)
+                call("avt_set_wgrad_tiles", 1)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
