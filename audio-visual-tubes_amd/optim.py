@@ -56,17 +56,25 @@ def _dense(t: torch.Tensor) -> bool:
 
 
 class FlatAdam:
-    """Adam state for the trainable region of a FlatStore: one kernel launch per step."""
+    """Adam state for the trainable region of a FlatStore.  The step count lives on the device
+    (``avt_adam_step_dev``), so a step is replayable from a captured HIP graph."""
 
     def __init__(self, flat, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4):
         self.flat = flat
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         n = flat.n_train
-        self.exp_avg = torch.zeros(n, device=flat.flat.device, dtype=torch.float32)
-        self.exp_avg_sq = torch.zeros(n, device=flat.flat.device, dtype=torch.float32)
-        self.t = 0
+        dev = flat.flat.device
+        self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.t_dev = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._coef = torch.zeros(2, device=dev, dtype=torch.float32)
+
+    @property
+    def t(self) -> int:
+        """Steps taken (host read: synchronises)."""
+        return int(self.t_dev.item())
 
     def step(self, gflat: torch.Tensor, grad_scale: float = 1.0):
-        self.t += 1
-        call("avt_adam_step", P(self.flat.flat), P(gflat), P(self.exp_avg), P(self.exp_avg_sq), self.flat.n_train,
-             grad_scale, self.lr, self.betas[0], self.betas[1], self.eps, self.wd, self.t, stream_ptr())
+        call("avt_adam_step_dev", P(self.flat.flat), P(gflat), P(self.exp_avg), P(self.exp_avg_sq),
+             self.flat.n_train, grad_scale, self.lr, self.betas[0], self.betas[1], self.eps, self.wd, P(self.t_dev),
+             P(self._coef), stream_ptr())

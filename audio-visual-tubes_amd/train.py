@@ -53,13 +53,59 @@ class HardWayTrainStep:
             # start from identical weights everywhere (DDP constructor semantics)
             dist.broadcast(self.flat.flat, 0, group=self.pg)
             sync_buffers(self.flat.bflat, self.pg)
+        self._graph = None
+        self._graph_opt = None
 
-    def step(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
-        """Returns the local mean CE loss (device scalar, no host sync)."""
-        sync_buffers(self.flat.bflat, self.pg)
+    def _fwd_bwd(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
         out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
         self.grad.zero_()
         self.engine.backward(tape, out["dlogits"], self.grad)
+        return out["loss"]
+
+    def step(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
+        """Returns the local mean CE loss (device scalar, no host sync)."""
+        if self._graph is not None:
+            return self._replay(image, audio)
+        sync_buffers(self.flat.bflat, self.pg)
+        loss = self._fwd_bwd(image, audio)
         scale = sync_gradients(self.grad, self.pg)
         self.opt.step(self.grad, grad_scale=scale)
-        return out["loss"]
+        return loss
+
+    def capture(self, image: torch.Tensor, audio: torch.Tensor) -> None:
+        """Record one step into HIP graph(s) (torch.cuda.CUDAGraph is hipGraph on ROCm) so that
+        later steps are replays: no per-kernel host launch cost and no launch gaps between the
+        ~700 kernels of a step.  World 1: one graph (fwd + CE + bwd + Adam).  World > 1: the RCCL
+        collectives stay eager between two graphs (fwd+bwd, then Adam).  ``image``/``audio``
+        become the static inputs; later steps copy theirs in unless they pass these tensors.
+        Call after at least one eager step (the engine allocates its buffers lazily).  Capture
+        records launches without running them, so it has no effect on the training state."""
+        torch.cuda.synchronize()
+        self._static_in = (image, audio)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._fwd_bwd(image, audio)
+            if self.world == 1:
+                self.opt.step(self.grad, grad_scale=1.0)
+        self._static_loss = loss
+        if self.world > 1:
+            g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_opt, pool=g.pool()):
+                self.opt.step(self.grad, grad_scale=1.0 / self.world)
+            self._graph_opt = g_opt
+        self._graph = g
+
+    def _replay(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
+        si, sa = self._static_in
+        if image is not si:
+            si.copy_(image)
+        if audio is not sa:
+            sa.copy_(audio)
+        if self.world > 1:
+            sync_buffers(self.flat.bflat, self.pg)
+            self._graph.replay()
+            sync_gradients(self.grad, self.pg)
+            self._graph_opt.replay()
+        else:
+            self._graph.replay()
+        return self._static_loss

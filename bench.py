@@ -78,6 +78,10 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="clips per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
+                    "captured HIP graph of the step")
+    ap.add_argument("--prof-steps", type=int, default=2, help="eager steps with HIP events around every conv "
+                    "launch after the timed region (roofline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,27 +106,38 @@ def main():
     B = args.batch
     img, aud = synthetic_inputs(B, dev, seed=1000 + rank)
 
-    for _ in range(args.warmup):
+    use_graph = not args.no_graph
+    for i in range(max(args.warmup, 1 if use_graph else 0)):
+        loss = step.step(img, aud)
+        if use_graph and i == 0:
+            step.capture(img, aud)  # later warm-up and all timed steps are graph replays
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
         loss = step.step(img, aud)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loss_v = float(loss)
+    # roofline of the conv family: HIP events on the launch stream around every conv launch of a
+    # few eager steps of the same workload (kept out of the timed region above)
+    eager = HardWayTrainStep.__new__(HardWayTrainStep)
+    eager.__dict__.update(step.__dict__)
+    eager._graph = None
     with ConvProfiler() as prof:
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            loss = step.step(img, aud)
+        for _ in range(args.prof_steps):
+            eager.step(img, aud)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
     conv = prof.summary()
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = el.item()
-    loss_v = float(loss)
     if rank == 0:
         clips = B * world * args.steps
         value = clips / elapsed
@@ -150,8 +165,11 @@ def main():
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
                          "launches": n_launch,
                          "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
-                                          "ms_per_step": round(v[2] / args.steps, 3)} for k, v in conv.items()},
-                         "conv_ms_per_step": round(ms / args.steps, 3)},
+                                          "ms_per_step": round(v[2] / args.prof_steps, 3)} for k, v in conv.items()},
+                         "conv_ms_per_step": round(ms / args.prof_steps, 3),
+                         "measured": f"HIP events around each conv launch, {args.prof_steps} eager steps after the "
+                                     "timed region"},
+            "launch": "eager" if args.no_graph else "hip-graph replay",
             "step_tflops_per_gpu": round(value / world * GFLOP_PER_CLIP / 1e3, 2),
             "step_mfma_frac": round(value / world * GFLOP_PER_CLIP / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
             "loss": round(loss_v, 6),

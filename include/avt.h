@@ -129,6 +129,11 @@ int avt_hardway_bwd(const void* v, const float* an, const float* inv, const floa
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, void* stream);
+/* avt_adam_step with the step count on the device (*step is incremented first) and the bias
+ * corrections computed there into coef[2] — graph-capturable */
+int avt_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                      float grad_scale, float lr, float beta1, float beta2, float eps, float weight_decay, int* step,
+                      float* coef, void* stream);
 int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
                          void* stream);
 /* two launches (fwd copy, dgrad transpose) for many convs: descs = device array of n records

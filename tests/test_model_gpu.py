@@ -157,6 +157,37 @@ def test_loss_decreases_over_steps():
     assert losses[-1] < losses[0], losses
 
 
+def test_graph_replay_matches_eager():
+    """A step captured into a HIP graph and replayed (new inputs copied into the static ones)
+    follows the eager steps: same losses, weights, BN buffers, Adam step count."""
+    data = [(orc.make_image(4, 64, seed=s), orc.make_spectrogram(4, 65, 76, seed=s)) for s in (1, 2, 3)]
+    m_e, m_g = _model(), _model()
+    s_e = HardWayTrainStep(m_e, lr=1e-6, weight_decay=1e-4)
+    s_g = HardWayTrainStep(m_g, lr=1e-6, weight_decay=1e-4)
+    le, lg = [], []
+    for i, (img, aud) in enumerate(data):
+        le.append(s_e.step(img.to(DEV), aud.to(DEV)).item())
+    for i, (img, aud) in enumerate(data):
+        img, aud = img.to(DEV), aud.to(DEV)
+        if i == 0:
+            lg.append(s_g.step(img, aud).item())
+            s_g.capture(img.clone(), aud.clone())
+        else:
+            lg.append(s_g.step(img, aud).item())
+    print("eager", le, "graph", lg)
+    np.testing.assert_allclose(lg, le, rtol=1e-4)
+    assert s_e.opt.t == s_g.opt.t == 3
+    sd_e, sd_g = m_e.state_dict(), m_g.state_dict()
+    for k in sd_e:
+        a, b = sd_e[k].double(), sd_g[k].double()
+        if k.endswith("num_batches_tracked"):
+            assert int(a) == int(b) == 3, k
+        elif "running" in k:
+            assert (a - b).abs().max().item() <= 1e-3 * max(1.0, a.abs().max().item()), k
+        else:  # <= lr per step; split-K / BN atomics can flip a ~0 gradient's update
+            assert (a - b).abs().max().item() <= 6.5e-6, k
+
+
 def test_eval_mode_uses_running_stats(golden_dir):
     g = _golden(golden_dir, "avenet_tiny_b4")
     img, aud = _inputs(g)
