@@ -151,7 +151,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   }
   const long long rbeg = (long long)blockIdx.x * rows_per_block;
   const long long rend = min(rows, rbeg + rows_per_block);
-  for (long long r = rbeg + r0; r < rend; r += rstep) {
+  // two rows per iteration: four independent 16-B loads in flight per thread
+  long long r = rbeg + r0;
+  for (; r + rstep < rend; r += 2 * rstep) {
+    const size_t o0 = (size_t)r * cv + chunk, o1 = o0 + (size_t)rstep * cv;
+    const u32x4 ga = reinterpret_cast<const u32x4*>(g)[o0], gb = reinterpret_cast<const u32x4*>(g)[o1];
+    const u32x4 xa = reinterpret_cast<const u32x4*>(xc)[o0], xb = reinterpret_cast<const u32x4*>(xc)[o1];
+    float g0[8], x0[8], g1[8], x1[8];
+    unpack8(ga, g0);
+    unpack8(xa, x0);
+    unpack8(gb, g1);
+    unpack8(xb, x1);
+    relu_mask8(g0, x0, y, o0, mscale, mshift, c0);
+    relu_mask8(g1, x1, y, o1, mscale, mshift, c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += g0[e] + g1[e];
+      s2[e] += g0[e] * (x0[e] - mu[e]) * is[e] + g1[e] * (x1[e] - mu[e]) * is[e];
+    }
+  }
+  if (r < rend) {
     const size_t off = (size_t)r * cv + chunk;
     float gg[8], xx[8];
     unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
@@ -256,8 +275,17 @@ __global__ __launch_bounds__(256) void stem_bn_relu_maxpool_fwd_kernel(
   const int row = blockIdx.x;  // n * P + p
   const int n = row / P, p = row - n * P;
   const int cv = 1 << cvs;
-  const int r_lo = p == 0 ? 1 : 0, r_hi = min(2, H - 1 - (2 * p - 1));
   const bf16_t* cimg = c + (size_t)n * H * W * C;
+  // window rows 2p-1+r, r = 0..2 (validity is block-uniform); loads use clamped coordinates and
+  // out-of-image taps are masked, so all nine 16-B loads of a thread issue together
+  bool rok[3];
+  int hh[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int h = p * 2 - 1 + r;
+    rok[r] = h >= 0 && h < H;
+    hh[r] = min(max(h, 0), H - 1);
+  }
   for (int t = threadIdx.x; t < Q * cv; t += 256) {
     const int q = t >> cvs, c8 = t & (cv - 1);
     float sc[8], sh[8], best[8], bc[8];
@@ -270,21 +298,29 @@ __global__ __launch_bounds__(256) void stem_bn_relu_maxpool_fwd_kernel(
       bc[e] = 0.f;
       bi[e] = 0;
     }
-    for (int r = r_lo; r <= r_hi; ++r) {
-      const int h = p * 2 - 1 + r;
-      for (int s = 0; s < 3; ++s) {
-        const int w = q * 2 - 1 + s;
-        if (w < 0 || w >= W) continue;
-        float xv[8];
-        unpack8(*reinterpret_cast<const u32x4*>(cimg + ((size_t)h * W + w) * C + c8 * 8), xv);
+    u32x4 v[9];
+    bool ok[9];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = bf2f(f2bf(fmaxf(__builtin_fmaf(xv[e], sc[e], sh[e]), 0.f)));
-          if (f > best[e] || f != f) {
-            best[e] = f;
-            bc[e] = xv[e];
-            bi[e] = r * 3 + s;
-          }
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int w = q * 2 - 1 + s2;
+        ok[r * 3 + s2] = rok[r] && w >= 0 && w < W;
+        const int wc = min(max(w, 0), W - 1);
+        v[r * 3 + s2] = *reinterpret_cast<const u32x4*>(cimg + ((size_t)hh[r] * W + wc) * C + c8 * 8);
+      }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!ok[k]) continue;
+      float xv[8];
+      unpack8(v[k], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = bf2f(f2bf(fmaxf(__builtin_fmaf(xv[e], sc[e], sh[e]), 0.f)));
+        if (f > best[e] || f != f) {
+          best[e] = f;
+          bc[e] = xv[e];
+          bi[e] = k;
         }
       }
     }
@@ -298,37 +334,82 @@ __global__ __launch_bounds__(256) void stem_bn_relu_maxpool_fwd_kernel(
   }
 }
 
+// LDS capacity for the two pooled rows a bwd block reads: 2 x Q x C x (2 B grad + 1 B argmax)
+constexpr int kStemLdsBytes = 48 * 1024;
+
 __global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
     const bf16_t* __restrict__ gy, const unsigned char* __restrict__ idx, const bf16_t* __restrict__ c,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ k1,
     const float* __restrict__ k2, bf16_t* __restrict__ gc, int H, int W, int C, int cvs, int P, int Q) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // 6*Q*C bytes (dynamic)
   const int row = blockIdx.x;  // n * H + h
   const int n = row / H, h = row - n * H;
   const int cv = 1 << cvs;
-  // pooled rows p with 2p-1 <= h <= 2p+1, and the window row kh = h - (2p-1) in each
-  const int p_lo = h >> 1, p_hi = min(P - 1, (h + 1) >> 1);
-  for (int t = threadIdx.x; t < W * cv; t += 256) {
+  // Windows covering input row h: p0 = h/2 (window row kh = 1 if h even, 2 if odd) and, for odd
+  // h, p0 + 1 (kh = 0); likewise for columns.  The block first stages those (<= 2) pooled rows of
+  // gy and argmax into LDS with coalesced 16-B copies, so each pooled element is fetched from
+  // memory once per block instead of once per covering input pixel.
+  const int p0 = h >> 1, kh0 = h - 2 * p0 + 1;
+  const bool p_two = (h & 1) && p0 + 1 < P;
+  const int np = p_two ? 2 : 1;
+  const int rowg = Q * C * 2, rowi = Q * C;  // bytes of one pooled row of gy / argmax
+  bf16_t* lg = reinterpret_cast<bf16_t*>(lds);
+  unsigned char* li = reinterpret_cast<unsigned char*>(lds + 2 * rowg);
+  for (int k = 0; k < np; ++k) {
+    const size_t prow = (size_t)n * P + p0 + k;
+    const u32x4* sg = reinterpret_cast<const u32x4*>(gy + prow * Q * C);
+    const u32x4* si = reinterpret_cast<const u32x4*>(idx + prow * Q * C);
+    for (int t = threadIdx.x; t < rowg / 16; t += 256) reinterpret_cast<u32x4*>(lg + k * Q * C)[t] = sg[t];
+    for (int t = threadIdx.x; t < rowi / 16; t += 256) reinterpret_cast<u32x4*>(li + k * rowi)[t] = si[t];
+  }
+  __syncthreads();
+  const int k1r = p_two ? 1 : 0;  // LDS row of the second window row (aliases the first if none)
+  // the pre-activations of this thread's (<= kStemItems) items are loaded before any is used:
+  // enough 16-B loads in flight per CU to stream c at HBM rate
+  constexpr int kStemItems = 6;
+  u32x4 cx[kStemItems];
+#pragma unroll
+  for (int j = 0; j < kStemItems; ++j) {
+    const int t = threadIdx.x + 256 * j;
+    if (t < W * cv) cx[j] = *reinterpret_cast<const u32x4*>(c + ((size_t)row * W) * C + (size_t)t * 8);
+  }
+#pragma unroll
+  for (int j = 0; j < kStemItems; ++j) {
+    const int t = threadIdx.x + 256 * j;
+    if (t >= W * cv) break;
     const int w = t >> cvs, c8 = t & (cv - 1);
-    float gg[8], xx[8], o[8];
+    const int q0 = w >> 1, kw0 = w - 2 * q0 + 1;
+    const bool q_two = (w & 1) && q0 + 1 < Q;
+    const int q1 = q_two ? q0 + 1 : q0;
+    const int e00 = q0 * C + c8 * 8, e01 = q1 * C + c8 * 8;
+    const int e10 = k1r * Q * C + e00, e11 = k1r * Q * C + e01;
+    const unsigned long long i00 = *reinterpret_cast<const unsigned long long*>(li + e00);
+    const unsigned long long i01 = *reinterpret_cast<const unsigned long long*>(li + e01);
+    const unsigned long long i10 = *reinterpret_cast<const unsigned long long*>(li + e10);
+    const unsigned long long i11 = *reinterpret_cast<const unsigned long long*>(li + e11);
+    // window position of (h, w) in each candidate; 0xff (never an argmax) where there is none
+    const int pos00 = kh0 * 3 + kw0;
+    const int pos01 = q_two ? kh0 * 3 + kw0 - 2 : 0xff;
+    const int pos10 = p_two ? (kh0 - 2) * 3 + kw0 : 0xff;
+    const int pos11 = (p_two && q_two) ? (kh0 - 2) * 3 + kw0 - 2 : 0xff;
+    float gg[8], xx[8], o[8], f00[8], f01[8], f10[8], f11[8];
+    unpack8(*reinterpret_cast<const u32x4*>(lg + e00), f00);
+    unpack8(*reinterpret_cast<const u32x4*>(lg + e01), f01);
+    unpack8(*reinterpret_cast<const u32x4*>(lg + e10), f10);
+    unpack8(*reinterpret_cast<const u32x4*>(lg + e11), f11);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) gg[e] = 0.f;
-    const int q_lo = w >> 1, q_hi = min(Q - 1, (w + 1) >> 1);
-    for (int p = p_lo; p <= p_hi; ++p) {
-      const int kh = h - (2 * p - 1);
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int pos = kh * 3 + (w - (2 * q - 1));
-        const size_t off = (((size_t)n * P + p) * Q + q) * C + c8 * 8;
-        const unsigned long long ib = *reinterpret_cast<const unsigned long long*>(idx + off);
-        float gv[8];
-        unpack8(*reinterpret_cast<const u32x4*>(gy + off), gv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if ((int)((ib >> (8 * e)) & 0xff) == pos) gg[e] += gv[e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      const int sh8 = 8 * e;
+      float a = 0.f;
+      a += ((int)((i00 >> sh8) & 0xff) == pos00) ? f00[e] : 0.f;
+      a += ((int)((i01 >> sh8) & 0xff) == pos01) ? f01[e] : 0.f;
+      a += ((int)((i10 >> sh8) & 0xff) == pos10) ? f10[e] : 0.f;
+      a += ((int)((i11 >> sh8) & 0xff) == pos11) ? f11[e] : 0.f;
+      gg[e] = a;
     }
     const size_t xo = ((size_t)row * W + w) * C + c8 * 8;
-    unpack8(*reinterpret_cast<const u32x4*>(c + xo), xx);
+    unpack8(cx[j], xx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int ch = c8 * 8 + e;
@@ -343,7 +424,7 @@ __global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
 static void bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* mscale, const float* mshift,
                                  const bf16_t* xc, const float* mean, const float* invstd, double* acc, long long rows,
                                  int C, hipStream_t st) {
-  // ~2 blocks per CU of rows
+  // ~2 blocks per CU of rows (more blocks measured slower: their fp64 atomics contend)
   long long rpb = (rows + 511) / 512;
   const int rstep = 256 / (C / 8);
   rpb = ((rpb + rstep - 1) / rstep) * rstep;
@@ -462,6 +543,8 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   AVT_REQUIRE(gy && idx && carg && c && scale && shift && mean && invstd && gamma && gc && workspace,
               "stem_maxpool_bn_relu_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "stem_maxpool_bn_relu_bwd: C=%d unsupported", C);
+  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)W * (C / 8) <= 6 * 256,
+              "stem_maxpool_bn_relu_bwd: W=%d C=%d too wide", W, C);
   AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_maxpool_bn_relu_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");
   const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
@@ -473,7 +556,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
                        (long long)N * P * Q, C, st);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
-  hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), 0, st, (const bf16_t*)gy,
+  hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), (size_t)6 * Q * C, st, (const bf16_t*)gy,
                      (const unsigned char*)idx, (const bf16_t*)c, scale, shift, mean, invstd, gamma, k1, k2,
                      (bf16_t*)gc, H, W, C, ilog2(C / 8), P, Q);
   return check_launch("stem_maxpool_bn_relu_bwd");
