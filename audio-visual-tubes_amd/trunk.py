@@ -33,7 +33,9 @@ def conv_out(n: int, k: int, s: int, p: int) -> int:
 
 class ConvProfiler:
     """Optional HIP-event bracketing of every conv launch (bench.py's live roofline).
-    Records (kind, algorithmic FLOPs, start, end) on the launching stream."""
+    Records (kind, algorithmic FLOPs, algorithmic HBM bytes, start, end) on the launching stream.
+    Algorithmic bytes = each operand read once + the output written once (fp32 wgrad output:
+    read-modify-write)."""
 
     active: Optional["ConvProfiler"] = None
 
@@ -57,23 +59,25 @@ class ConvProfiler:
         return ev
 
     @staticmethod
-    def end(ev, kind: str, flops: float):
+    def end(ev, kind: str, flops: float, nbytes: float = 0.0):
         p = ConvProfiler.active
         if p is None or ev is None:
             return
         e2 = torch.cuda.Event(enable_timing=True)
         e2.record()
-        p.records.append((kind, flops, ev, e2))
+        p.records.append((kind, flops, nbytes, ev, e2))
 
     def summary(self):
+        """kind -> [launches, FLOPs, ms, algorithmic bytes]"""
         torch.cuda.synchronize()
         out = {}
-        for kind, fl, a, b in self.records:
+        for kind, fl, nb, a, b in self.records:
             ms = a.elapsed_time(b)
-            k = out.setdefault(kind, [0, 0.0, 0.0])
+            k = out.setdefault(kind, [0, 0.0, 0.0, 0.0])
             k[0] += 1
             k[1] += fl
             k[2] += ms
+            k[3] += nb
         return out
 
 
@@ -189,7 +193,8 @@ class Trunk:
         ev = ConvProfiler.begin()
         call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
              spec.stride, spec.pad, spec.kg, stream_ptr())
-        ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin)
+        ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin,
+                         2.0 * (x.numel() + wf.numel() + y.numel()))
         stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training)
         return y, stats, Pq, Qq
 
@@ -258,7 +263,8 @@ class Trunk:
         ev = ConvProfiler.begin()
         call("avt_conv2d_wgrad", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
              spec.stride, spec.pad, P(ws), wsb, stream_ptr())
-        ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin)
+        ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
+                         2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
 
     def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None):
         _, wt = store.packed(spec)
@@ -266,7 +272,8 @@ class Trunk:
         ev = ConvProfiler.begin()
         call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
              spec.stride, spec.pad, stream_ptr())
-        ConvProfiler.end(ev, "dgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin)
+        ConvProfiler.end(ev, "dgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
+                         2.0 * (gy.numel() + wt.numel() + gx.numel() * (2 if add is not None else 1)))
         return gx
 
     def backward(self, tape: Dict, g_out: torch.Tensor, store: Store):

@@ -40,6 +40,23 @@ def synthetic_inputs(B, device, seed):
     return img, spec
 
 
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "conv_traffic_b128.json")
+
+
+def conv_traffic(launches_per_step, B, world):
+    """HBM bytes per conv launch from the committed PMC summary (tools/pmc_traffic.sh ->
+    tools/traffic_summary.py --json) of this same workload; None if absent or for another batch."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("per_gpu_batch") != B or launches_per_step <= 0:
+        return None, None
+    per_step = t["conv_read_bytes_per_step"] + t["conv_write_bytes_per_step"]
+    return round(per_step / launches_per_step), os.path.relpath(TRAFFIC_FILE, REPO)
+
+
 def cpu_baseline(budget_s: float = 20.0):
     """Oracle (fp32 PyTorch CPU restatement) full train step at B=2 on the host cores."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -144,7 +161,9 @@ def main():
         fl = sum(v[1] for v in conv.values())
         ms = sum(v[2] for v in conv.values())
         n_launch = sum(v[0] for v in conv.values())
+        alg_bytes = sum(v[3] for v in conv.values())
         achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        traffic, traffic_src = conv_traffic(n_launch / max(args.prof_steps, 1), B, world)
         rec = {
             "metric": "train-step clips/sec (whole node), ResNet18 vision + ResNet18 audio hard-way loss",
             "value": round(value, 2),
@@ -162,11 +181,15 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM (fwd+dgrad+wgrad)",
                          "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per conv launch (PMC FETCH_SIZE/WRITE_SIZE, gfx950-corrected)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": round(alg_bytes / max(n_launch, 1)),
+                         "algorithmic_flops_per_launch": round(fl / max(n_launch, 1)),
                          "launches": n_launch,
                          "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
-                                          "ms_per_step": round(v[2] / args.prof_steps, 3)} for k, v in conv.items()},
-                         "conv_ms_per_step": round(ms / args.prof_steps, 3),
+                                          "ms_per_step": round(v[2] / max(args.prof_steps, 1), 3)} for k, v in conv.items()},
+                         "conv_ms_per_step": round(ms / max(args.prof_steps, 1), 3),
                          "measured": f"HIP events around each conv launch, {args.prof_steps} eager steps after the "
                                      "timed region"},
             "launch": "eager" if args.no_graph else "hip-graph replay",

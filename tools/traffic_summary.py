@@ -1,0 +1,72 @@
+"""Per-kernel HBM bytes from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+FETCH_SIZE and WRITE_SIZE are reported in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM):
+FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) streaming reads, so read bytes =
+2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B stores and dword atomics.  The Adam kernel
+(known bytes: 16 B/param read, 12 B/param written) is printed as the calibration check.
+
+usage: python tools/traffic_summary.py <dir with FETCH_SIZE/ WRITE_SIZE/> <steps in the run> [--json out] [--batch B]
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+CONV = ("conv_nt_pipe_kernel", "conv_tn_pipe_kernel", "gemm_nt_kernel", "gemm_tn_kernel",
+        "wgrad_slab_reduce_kernel")
+
+
+def load(d, ctr):
+    tot, cnt = defaultdict(float), defaultdict(int)
+    for path in glob.glob(f"{d}/{ctr}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] != ctr:
+                continue
+            k = r["Kernel_Name"]
+            tot[k] += float(r["Counter_Value"])
+            cnt[k] += 1
+    return tot, cnt
+
+
+def main():
+    d, steps = sys.argv[1], float(sys.argv[2])
+    fetch, nf = load(d, "FETCH_SIZE")
+    write, _ = load(d, "WRITE_SIZE")
+    rows = []
+    for k in set(fetch) | set(write):
+        rd = 2.0 * fetch.get(k, 0.0) * 1024.0
+        wr = write.get(k, 0.0) * 1024.0
+        rows.append((k, nf.get(k, 0), rd, wr))
+    rows.sort(key=lambda r: -(r[2] + r[3]))
+    conv_rd = conv_wr = 0.0
+    conv_n = 0
+    for k, n, rd, wr in rows:
+        if any(c in k for c in CONV):
+            conv_rd += rd
+            conv_wr += wr
+            conv_n += n
+    for k, n, rd, wr in rows[:40]:
+        print(f"{(rd + wr) / 1e9 / steps:8.3f} GB/step  read {rd / 1e9 / steps:7.3f}  write {wr / 1e9 / steps:7.3f}  "
+              f"n={n / steps:6.1f}/step  {k[:90]}")
+    print(f"conv family: {conv_n / steps:.0f} dispatches/step, read {conv_rd / 1e9 / steps:.3f} GB/step, "
+          f"write {conv_wr / 1e9 / steps:.3f} GB/step, {(conv_rd + conv_wr) / max(conv_n, 1) / 1e6:.3f} MB/dispatch")
+    for k, n, rd, wr in rows:
+        if "adam_kernel" in k:
+            print(f"calibration adam: read {rd / n / 1e6:.1f} MB/launch, write {wr / n / 1e6:.1f} MB/launch "
+                  f"(algorithmic: 357.5 read / 268.2 write for 22,346,752 params)")
+    if "--json" in sys.argv:
+        out = sys.argv[sys.argv.index("--json") + 1]
+        batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 128
+        json.dump({"per_gpu_batch": batch, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py "
+                   "--no-graph (tools/pmc_traffic.sh); read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB",
+                   "conv_dispatches_per_step": conv_n / steps, "conv_read_bytes_per_step": conv_rd / steps,
+                   "conv_write_bytes_per_step": conv_wr / steps,
+                   "conv_bytes_per_dispatch": (conv_rd + conv_wr) / max(conv_n, 1),
+                   "per_kernel": {k[:120]: {"dispatches_per_step": n / steps, "read_bytes_per_step": rd / steps,
+                                            "write_bytes_per_step": wr / steps} for k, n, rd, wr in rows}},
+                  open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
