@@ -14,7 +14,9 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libavt.so")
-SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip"]
+# A/B measurement only: load another in-tree build of the same ABI (e.g. libavt_base.so)
+LOAD_PATH = os.environ.get("AVT_LIB_PATH", LIB_PATH)
+SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip", "tube.hip"]
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -39,6 +41,12 @@ SIGNATURES = {
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),
     "avt_bn_finalize": (_I, [_P, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
+    "avt_bn_finalize_rep": (_I, [_P, _L, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
+    "avt_conv3d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_video_stem_im2col": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_pack_conv3d_weight": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_repeat_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),
+    "avt_sum_rep_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),
     "avt_bn_apply": (_I, [_P, _P, _P, _P, _P, _P, _P, _L, _I, _I, _P]),
     "avt_bn_bwd_workspace": (_Z, [_L, _I]),
     "avt_bn_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
@@ -90,10 +98,12 @@ def lib() -> ctypes.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(f"libavt.so not built ({LIB_PATH}); run __graft_entry__.build()")
-            h = ctypes.CDLL(LIB_PATH)
+            if not os.path.exists(LOAD_PATH):
+                raise RuntimeError(f"libavt.so not built ({LOAD_PATH}); run __graft_entry__.build()")
+            h = ctypes.CDLL(LOAD_PATH)
             for name, (res, args) in SIGNATURES.items():
+                if LOAD_PATH != LIB_PATH and not hasattr(h, name):
+                    continue  # an older A/B build
                 fn = getattr(h, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -39,7 +39,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ a
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, float momentum, float eps, float* scale,
-                                                          float* shift, float* save_mean, float* save_invstd) {
+                                                          float* shift, float* save_mean, float* save_invstd,
+                                                          long long rep) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double S = 0.0, Q = 0.0, R = 0.0;
@@ -65,7 +66,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ a
   if (save_mean) save_mean[c] = (float)mean;
   if (save_invstd) save_invstd[c] = inv;
   if (running_mean) {
-    const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
+    // unbiased variance of the logical batch, in which each accumulated row occurs `rep` times
+    const double nl = n * (double)rep;
+    const float unb = nl > 1.0 ? (float)(m2 * (double)rep / (nl - 1.0)) : var;
     running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
   }
@@ -446,8 +449,23 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
-                     beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd);
+                     beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
+}
+
+// As avt_bn_finalize for a logical batch in which every accumulated row occurs `rep` times (the
+// tube step's t-fold repeated spectrogram, train_3D.py:128-130, run once per distinct clip):
+// mean and biased variance are those of the distinct rows; the running variance gets the
+// unbiased factor of the rows*rep logical rows, exactly as BatchNorm2d over the repeated batch.
+extern "C" int avt_bn_finalize_rep(double* acc, long long rows, long long rep, int C, const float* gamma,
+                                   const float* beta, float* running_mean, float* running_var, float momentum,
+                                   float eps, float* scale, float* shift, float* save_mean, float* save_invstd,
+                                   void* stream) {
+  AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize_rep: null pointer");
+  AVT_REQUIRE(rows > 0 && C > 0 && rep >= 1, "bn_finalize_rep: empty input");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+                     beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, rep);
+  return check_launch("bn_finalize_rep");
 }
 
 extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual,

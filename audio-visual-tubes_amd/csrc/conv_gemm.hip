@@ -30,6 +30,8 @@ struct GemmNTParams {
   int M, Ng, Kg;
   int IH, IW, IC;      // source tensor geometry
   int OH, OW;          // pixel grid of the GEMM rows
+  int IT, OT;          // temporal extent of source / rows (Conv3d, temporal stride 1; 1 for Conv2d)
+  int KT, pad_t;       // temporal taps and padding (Conv3d; 1 / 0 for Conv2d)
   int R, S, stride, pad;
 };
 
@@ -530,12 +532,18 @@ extern "C" int avt_set_wgrad_tiles(int big) {
 static inline int conv_out(int in, int k, int st, int pad) { return (in + 2 * pad - k) / st + 1; }
 
 template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK>
-static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgs& ta, hipStream_t st) {
+static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgsV& ta, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
-  if (grid > 0)
+  if (grid <= 0) return;
+  if (p.IT > 1 || p.OT > 1 || ta.ntaps > 32) {  // Conv3d / the folded 49-tap video stem
+    if constexpr (MODE == MODE_FWD)
+      hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK, true>), dim3(grid), dim3(WM * WN * 64), 0,
+                         st, p, ta);
+  } else {
     hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK>), dim3(grid), dim3(WM * WN * 64), 0, st, p,
-                       ta);
+                       narrow_args(ta));
+  }
 }
 
 // Builds the tap list(s) and launches: fwd / stride-1 dgrad in one launch; a stride-2 dgrad as
@@ -546,19 +554,21 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
     launch_glds<MODE, 2, 2, 2, (WN * TN * 32) / 64, 3, 32>(p, st);  // 4-wave k32 tile of the same width
     return;
   }
-  NTPipeArgs ta{};
-  const int batch = p.M / (p.OH * p.OW);
-  ta.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * p.IC * 2);
+  NTPipeArgsV ta{};
+  const int batch = p.M / (p.OT * p.OH * p.OW);
+  ta.act_bytes = (unsigned)((size_t)batch * p.IT * p.IH * p.IW * p.IC * 2);
   ta.w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
   if (MODE == MODE_FWD || p.stride == 1) {
-    ta.ntaps = p.R * p.S;
-    for (int r = 0; r < p.R; ++r)
-      for (int s = 0; s < p.S; ++s) {
-        const int t = r * p.S + s;
-        ta.tap_w[t] = t;
-        ta.tap_dy[t] = MODE == MODE_FWD ? r - p.pad : p.pad - r;
-        ta.tap_dx[t] = MODE == MODE_FWD ? s - p.pad : p.pad - s;
-      }
+    ta.ntaps = p.KT * p.R * p.S;
+    for (int kt = 0; kt < p.KT; ++kt)
+      for (int r = 0; r < p.R; ++r)
+        for (int s = 0; s < p.S; ++s) {
+          const int t = (kt * p.R + r) * p.S + s;
+          ta.tap_w[t] = t;
+          ta.tap_dt[t] = MODE == MODE_FWD ? kt - p.pad_t : p.pad_t - kt;
+          ta.tap_dy[t] = MODE == MODE_FWD ? r - p.pad : p.pad - r;
+          ta.tap_dx[t] = MODE == MODE_FWD ? s - p.pad : p.pad - s;
+        }
     launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(p, ta, st);
     return;
   }
@@ -567,7 +577,7 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
   ta.OWf = p.OW;
   for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
-      NTPipeArgs tc = ta;
+      NTPipeArgsV tc = ta;
       tc.ph = ph;
       tc.pw = pw;
       tc.ntaps = 0;
@@ -633,6 +643,7 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   AVT_REQUIRE(Kg % 32 == 0 && Kg >= R * S * Cp, "conv2d_fwd: Kg=%d must be a multiple of 32 >= R*S*C", Kg);
   AVT_REQUIRE(Cp % 32 == 0 || Cp == 4 || Cp == 1, "conv2d_fwd: C=%d unsupported (need %%32, or stem 1/4)", Cp);
   AVT_REQUIRE(Cp % 32 != 0 || Kg == R * S * Cp, "conv2d_fwd: Kg must equal R*S*C for C%%32==0");
+  AVT_REQUIRE(Cp % 32 != 0 || R * S <= kMaxTaps, "conv2d_fwd: at most %d taps for C%%32==0", kMaxTaps);
   AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_fwd: stride must be 1 or 2");
   GemmNTParams p{};
   p.act = (const bf16_t*)x;
@@ -643,7 +654,11 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   p.IH = H; p.IW = W; p.IC = Cp;
   p.OH = conv_out(H, R, stride, pad);
   p.OW = conv_out(W, S, stride, pad);
+  p.IT = p.OT = p.KT = 1;
+  p.pad_t = 0;
   p.M = N * p.OH * p.OW;
+  AVT_REQUIRE((size_t)N * H * W * Cp * 2 < (1ull << 31) && (size_t)p.M * K * 2 < (1ull << 31),
+              "conv2d_fwd: activation tensors must stay below 2 GiB (32-bit buffer offsets)");
   p.Ng = K;
   p.Kg = Kg;
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
@@ -666,6 +681,7 @@ extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const 
   AVT_REQUIRE(dy && wt && dx, "conv2d_dgrad: null pointer");
   AVT_REQUIRE(C % 64 == 0 && K % 32 == 0, "conv2d_dgrad: C=%d K=%d unsupported", C, K);
   AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
+  AVT_REQUIRE(R * S <= 32, "conv2d_dgrad: at most 32 taps");
   GemmNTParams p{};
   p.act = (const bf16_t*)dy;
   p.wmat = (const bf16_t*)wt;
@@ -676,7 +692,11 @@ extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const 
   p.IW = conv_out(W, S, stride, pad);
   p.IC = K;
   p.OH = H; p.OW = W;
+  p.IT = p.OT = p.KT = 1;
+  p.pad_t = 0;
   p.M = N * H * W;
+  AVT_REQUIRE((size_t)p.M * C * 2 < (1ull << 31) && (size_t)N * p.IH * p.IW * K * 2 < (1ull << 31),
+              "conv2d_dgrad: activation tensors must stay below 2 GiB (32-bit buffer offsets)");
   p.Ng = C;
   p.Kg = R * S * K;
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
@@ -686,6 +706,44 @@ extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const 
   else
     launch_nt<MODE_DGRAD, 8, 128, 64>(p, st);
   return check_launch("conv2d_dgrad");
+}
+
+// Conv3d forward (the R3D-18 video trunk, models/resnet3D.py:14-28 conv3x3x3 / conv1x1x1, called
+// from BasicBlock.forward 45-61): x NDHWC bf16 [N][T][H][W][Cp], wpack bf16 [K][(kt,r,s,c)],
+// y NDHWC bf16 [N][T'][H'][W'][K] with T' = T + 2*pad_t - KT + 1 (temporal stride 1, as every
+// Conv3d of the R3D-18 built by model.py:20 after the stem) and spatial stride `stride`.
+// BN statistics are accumulated in the epilogue exactly as conv2d_fwd.
+extern "C" int avt_conv3d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int T, int H, int W,
+                              int Cp, int K, int KT, int R, int S, int stride, int pad_t, int pad, void* stream) {
+  AVT_REQUIRE(x && wpack && y, "conv3d_fwd: null pointer");
+  AVT_REQUIRE(K % 64 == 0, "conv3d_fwd: K=%d must be a multiple of 64", K);
+  AVT_REQUIRE(Cp % 32 == 0, "conv3d_fwd: C=%d must be a multiple of 32", Cp);
+  AVT_REQUIRE(KT * R * S <= kMaxTaps && KT >= 1 && R >= 1 && S >= 1, "conv3d_fwd: at most %d taps", kMaxTaps);
+  AVT_REQUIRE(stride == 1 || stride == 2, "conv3d_fwd: spatial stride must be 1 or 2");
+  GemmNTParams p{};
+  p.act = (const bf16_t*)x;
+  p.wmat = (const bf16_t*)wpack;
+  p.out = (bf16_t*)y;
+  p.add = nullptr;
+  p.stats = bn_acc;
+  p.IT = T; p.IH = H; p.IW = W; p.IC = Cp;
+  p.OT = T + 2 * pad_t - KT + 1;
+  p.OH = conv_out(H, R, stride, pad);
+  p.OW = conv_out(W, S, stride, pad);
+  AVT_REQUIRE(p.OT >= 1 && p.OH >= 1 && p.OW >= 1, "conv3d_fwd: empty output");
+  p.M = N * p.OT * p.OH * p.OW;
+  p.Ng = K;
+  p.Kg = KT * R * S * Cp;
+  p.KT = KT; p.R = R; p.S = S; p.stride = stride; p.pad = pad; p.pad_t = pad_t;
+  AVT_REQUIRE((size_t)N * T * H * W * Cp * 2 < (1ull << 31) && (size_t)p.M * K * 2 < (1ull << 31),
+              "conv3d_fwd: activation tensors must stay below 2 GiB (32-bit buffer offsets)");
+  AVT_REQUIRE(conv_variant() == 1, "conv3d_fwd: needs the LDS-DMA conv kernels (AVT_CONV_VARIANT=1)");
+  hipStream_t st = (hipStream_t)stream;
+  if (K % 128 == 0)
+    launch_nt<MODE_FWD, 8, 128, 128>(p, st);
+  else
+    launch_nt<MODE_FWD, 8, 128, 64>(p, st);
+  return check_launch("conv3d_fwd");
 }
 
 // wgrad launch plan: tile shape, split-K and (pipelined kernel) the fp32 partial slab it needs.

@@ -12,6 +12,7 @@
 // k-tile (tiles past the end are issued as all-OOB dummies so the count is constant), XCD-aware
 // tile order.
 #pragma once
+#include <type_traits>
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -31,15 +32,41 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_w
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_wave_base, 16, voff, 0, 0, 0);
 }
 
-struct NTPipeArgs {
+constexpr int kMaxTaps = 49;  // 7x7 (the R3D stem as a 32-channel Conv2d); 3x3x3 Conv3d needs 27
+
+template <int NTAPS>
+struct NTPipeArgsT {
   unsigned act_bytes, w_bytes;
-  int ntaps;              // taps in the K loop
-  int tap_w[9];           // weight tap index r*S+s of each listed tap
-  int tap_dy[9], tap_dx[9];  // source displacement of each tap relative to the row origin
+  int ntaps;              // taps in the K loop (<= NTAPS)
+  int tap_w[NTAPS];       // weight tap index ((kt*R)+r)*S+s of each listed tap
+  int tap_dt[NTAPS], tap_dy[NTAPS], tap_dx[NTAPS];  // source displacement of each tap relative to
+                                                    // the row origin
   int cls;                // 1: rows are one parity class of a stride-2 dgrad output
   int ph, pw;             // that class
   int OHf, OWf;           // full output grid (class mode)
 };
+typedef NTPipeArgsT<9> NTPipeArgs;          // Conv2d (3x3 and 1x1)
+typedef NTPipeArgsT<kMaxTaps> NTPipeArgsV;  // Conv3d 3x3x3 and the folded 7x7 video stem
+
+// the 2-D kernels take the 9-tap argument block (the larger one measured ~1.3 % slower on them)
+inline NTPipeArgs narrow_args(const NTPipeArgsV& v) {
+  NTPipeArgs a{};
+  a.act_bytes = v.act_bytes;
+  a.w_bytes = v.w_bytes;
+  a.ntaps = v.ntaps;
+  for (int t = 0; t < v.ntaps && t < 9; ++t) {
+    a.tap_w[t] = v.tap_w[t];
+    a.tap_dt[t] = v.tap_dt[t];
+    a.tap_dy[t] = v.tap_dy[t];
+    a.tap_dx[t] = v.tap_dx[t];
+  }
+  a.cls = v.cls;
+  a.ph = v.ph;
+  a.pw = v.pw;
+  a.OHf = v.OHf;
+  a.OWf = v.OWf;
+  return a;
+}
 
 // byte offset of 16-B chunk `chunk` of row `row` in a [rows][RB bytes] LDS image: the chunk is
 // XOR-swizzled by the row so that the 32 rows of an MFMA fragment read hit distinct banks
@@ -51,8 +78,13 @@ __device__ __forceinline__ int swz_rb(int row, int chunk) {
 
 // 4 or 8 waves as WM x WN, each wave TM x TN tiles of 32x32: BM = WM*TM*32, BN = WN*TN*32; BK = k-tile
 // depth (32 or 64 bf16: 64-B or whole 128-B lines per gathered row and tap).
-template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32>
-__global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams p, NTPipeArgs ta) {
+// VID: rows carry a temporal coordinate and the tap list may exceed 32 taps (the Conv3d of the
+// R3D-18 video trunk and its 49-tap stem); the Conv2d instances keep the 32-bit mask and 2-D row
+// decode (measured: the general form costs the 2-D convs ~3.5 %).
+template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32, bool VID = false>
+__global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
+    GemmNTParams p, typename std::conditional<VID, NTPipeArgsV, NTPipeArgs>::type ta) {
+  typedef typename std::conditional<VID, unsigned long long, unsigned>::type mask_t;
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(BK == 32 || BK == 64, "BK");
@@ -83,8 +115,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
 
   // ---- per-lane gather rows: instruction i of this wave covers rows (wid*AR + i)*RPI + lane/CPR ----
   const int lrow = lane / CPR, pchunk = lane % CPR;
-  unsigned a_off0[AR], a_mask[AR];
+  unsigned a_off0[AR];
+  mask_t a_mask[AR];
   const int hw = p.OH * p.OW;
+  const int thw = p.OT * hw;  // rows per sample: (t,) h, w  (OT = IT = 1 for Conv2d)
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int row = (wid * AR + i) * RPI + lrow;
@@ -92,7 +126,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
     const int m = m0 + row;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
-    const int n = mm / hw, rem = mm - n * hw;
+    int n, ot, rem;
+    if constexpr (VID) {
+      n = mm / thw;
+      const int rem0 = mm - n * thw;
+      ot = rem0 / hw;  // temporal stride 1: the row origin's t is ot
+      rem = rem0 - ot * hw;
+    } else {
+      n = mm / hw;
+      ot = 0;
+      rem = mm - n * hw;
+    }
     const int oh = rem / p.OW, ow = rem - oh * p.OW;
     int yb, xb;  // source coordinate of the row origin; tap t reads (yb + tap_dy[t], xb + tap_dx[t])
     if (MODE == MODE_FWD) {
@@ -102,14 +146,21 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
       yb = oh;  // class / stride-1 grids: displacements carry pad and parity
       xb = ow;
     }
-    unsigned mask = 0;
+    mask_t mask = 0;
     for (int t = 0; t < ta.ntaps; ++t) {
       const int y = yb + ta.tap_dy[t], x = xb + ta.tap_dx[t];
-      const bool v = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
-      mask |= (v ? 1u : 0u) << t;
+      bool v = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
+      if constexpr (VID) {
+        const int tt = ot + ta.tap_dt[t];
+        v = v && tt >= 0 && tt < p.IT;
+      }
+      mask |= (v ? (mask_t)1 : (mask_t)0) << t;
     }
     a_mask[i] = mask;
-    a_off0[i] = (unsigned)(((long long)n * p.IH * p.IW + (long long)yb * p.IW + xb) * p.IC + lc * 8) * 2u;
+    if constexpr (VID)
+      a_off0[i] = (unsigned)(((((long long)n * p.IT + ot) * p.IH + yb) * p.IW + xb) * p.IC + lc * 8) * 2u;
+    else
+      a_off0[i] = (unsigned)(((long long)n * p.IH * p.IW + (long long)yb * p.IW + xb) * p.IC + lc * 8) * 2u;
   }
   unsigned b_off[BR];
 #pragma unroll
@@ -126,7 +177,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
   // also drain the LDS fragment reads, on the loop's critical path).
   int lane_tapoff = 0, lane_tapw = 0;
   if (lane < ta.ntaps) {
-    lane_tapoff = (ta.tap_dy[lane] * p.IW + ta.tap_dx[lane]) * p.IC * 2;
+    const int dt = VID ? ta.tap_dt[lane] : 0;
+    lane_tapoff = ((dt * p.IH + ta.tap_dy[lane]) * p.IW + ta.tap_dx[lane]) * p.IC * 2;
     lane_tapw = ta.tap_w[lane] * p.IC * 2;
   }
 
@@ -142,7 +194,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const unsigned voff = a_off0[i] + (unsigned)tapoff;
-      buf_lds16(rsa, As + (wid * AR + i) * 1024, (live && ((a_mask[i] >> t) & 1u)) ? voff : kOOB);
+      const bool valid = VID ? (a_mask[i] & (mask_t)1) != 0 : ((a_mask[i] >> t) & 1u) != 0;
+      buf_lds16(rsa, As + (wid * AR + i) * 1024, (live && valid) ? voff : kOOB);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
@@ -152,6 +205,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(GemmNTParams
     if (it_c == p.IC) {
       it_c = 0;
       ++it_t;
+      if constexpr (VID) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) a_mask[i] >>= 1;  // bit 0 = validity of the next tap
+      }
     }
   };
 

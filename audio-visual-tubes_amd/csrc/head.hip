@@ -334,24 +334,28 @@ extern "C" int avt_hardway_ce(const float* logits, int B, int L, float scale, fl
 
 // Backward from dlogits to the trunk outputs.
 //   workspace: dA0 [B][P][B] fp32 + dvh [B][P][C] fp32
-//   outputs: gv [B][P][C] bf16 (grad of the vision layer4 map), gan [B][C] fp32 (grad of the unit audio vectors)
+//   outputs: gv [B][P][C] bf16 (grad of the vision layer4 map; dvh = gv = NULL skips it), gan [B][C] fp32
+//   (grad of the unit audio vectors)
 extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
                                const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
                                int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream) {
-  AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && dvh && gv && gan, "hardway_bwd: null pointer");
+  AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && gan, "hardway_bwd: null pointer");
+  AVT_REQUIRE((dvh == nullptr) == (gv == nullptr), "hardway_bwd: dvh and gv must be both set or both null");
   hipStream_t st = (hipStream_t)stream;
   const int rows = B * P;
   hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2, tau,
                      trimap, use_neg, dA0);
-  // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]
-  sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
+  // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]   (skipped when the vision map is detached:
+  // the tube head, whose video features come from a detached forward hook, model.py:12-15)
+  if (gv != nullptr) sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
   // gan[j][c] = sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
   (void)hipMemsetAsync(gan, 0, (size_t)B * C * sizeof(float), st);
   int splits = rows / 256;
   if (splits < 1) splits = 1;
   if (splits > 64) splits = 64;
   sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st);
-  hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
-                     (bf16_t*)gv, rows, C);
+  if (gv != nullptr)
+    hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
+                       (bf16_t*)gv, rows, C);
   return check_launch("hardway_bwd");
 }

@@ -1,0 +1,155 @@
+// Layout kernels of the 3-D tube path (FullModel, model.py:17-36; R3D-18 = models/resnet3D.py).
+//
+//  * Video stem as a 2-D conv.  The R3D stem Conv3d(3, 64, (7,7,7), stride (1,2,2), pad (3,3,3))
+//    (resnet3D.py:122-127) has temporal stride 1, so folding its 7 temporal taps into channels,
+//      X'[n][t][h][w][kt*4 + c] = x[n][c][t + kt - 3][h][w]   (0 outside the clip, c = 3 and
+//                                                              channels 28..31 zero),
+//    turns it into a Conv2d 7x7/s2/p3 with 32 channels over the N*T frames, which runs on the
+//    same LDS-DMA MFMA kernel as every other conv (C % 32 == 0).  The weight is packed to match:
+//      W'[k][(r*7 + s)*32 + kt*4 + c] = w[k][c][kt][r][s].
+//  * Conv3d weight packing: fp32 OIDHW (the Parameter layout) -> bf16 [K][(kt,r,s,c)], the fwd
+//    operand of avt_conv3d_fwd.
+#include "avt_common.h"
+
+namespace avt {
+
+// one thread per output pixel (n, t, h, w): 32 channels = 64 contiguous bytes
+__global__ __launch_bounds__(256) void video_stem_im2col_kernel(const float* __restrict__ x, bf16_t* __restrict__ out,
+                                                                int N, int C, int T, int HW, int KT, int pad_t) {
+  const long long npix = (long long)N * T * HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int hw = (int)(i % HW);
+    const long long nt = i / HW;
+    const int t = (int)(nt % T), n = (int)(nt / T);
+    float v[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      if (kt >= KT) break;
+      const int tt = t + kt - pad_t;
+      if (tt < 0 || tt >= T) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < C) v[kt * 4 + c] = x[(((long long)n * C + c) * T + tt) * HW + hw];
+    }
+    u32x4* o = reinterpret_cast<u32x4*>(out + i * 32);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      u32x4 w;
+      w[0] = pack2(v[q * 8 + 0], v[q * 8 + 1]);
+      w[1] = pack2(v[q * 8 + 2], v[q * 8 + 3]);
+      w[2] = pack2(v[q * 8 + 4], v[q * 8 + 5]);
+      w[3] = pack2(v[q * 8 + 6], v[q * 8 + 7]);
+      o[q] = w;
+    }
+  }
+}
+
+// fold = 0: out[k][((kt*R + r)*S + s)*C + c] = w[k][c][kt][r][s]            (Kg = KT*R*S*C)
+// fold = 1: out[k][(r*S + s)*32 + kt*4 + c] = w[k][c][kt][r][s], zero padded (Kg = R*S*32)
+__global__ __launch_bounds__(256) void pack_conv3d_kernel(const float* __restrict__ w, bf16_t* __restrict__ out, int K,
+                                                          int C, int KT, int R, int S, int fold, long long total) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int kg = fold ? R * S * 32 : KT * R * S * C;
+    const int k = (int)(i / kg), j = (int)(i % kg);
+    int kt, r, s, c;
+    bool ok = true;
+    if (fold) {
+      const int rs = j / 32, q = j % 32;
+      r = rs / S;
+      s = rs % S;
+      kt = q / 4;
+      c = q % 4;
+      ok = kt < KT && c < C;
+    } else {
+      c = j % C;
+      const int t = j / C;
+      s = t % S;
+      r = (t / S) % R;
+      kt = t / (S * R);
+    }
+    const float v = ok ? w[((((long long)k * C + c) * KT + kt) * R + r) * S + s] : 0.f;
+    out[i] = f2bf(v);
+  }
+}
+
+// out[(b*rep + k)][c] = in[b][c]  (the per-clip audio vector of each of its t frames)
+__global__ __launch_bounds__(256) void repeat_rows_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
+                                                          int rep, int C) {
+  const long long n = (long long)B * rep * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long row = i / C;
+    out[i] = in[(row / rep) * C + c];
+  }
+}
+
+// out[b][c] = sum_k in[(b*rep + k)][c]  (adjoint of repeat_rows_kernel)
+__global__ __launch_bounds__(256) void sum_rep_rows_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
+                                                           int rep, int C) {
+  const long long n = (long long)B * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long b = i / C;
+    float a = 0.f;
+    for (int k = 0; k < rep; ++k) a += in[(b * rep + k) * C + c];
+    out[i] = a;
+  }
+}
+
+static int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace avt
+
+using namespace avt;
+
+// x: fp32 NCDHW [N][C][T][H][W] (the reference's frames.float(), train_3D.py:131), C <= 4,
+// KT <= 7 -> out: bf16 [N][T][H][W][32] (see the file comment).
+extern "C" int avt_video_stem_im2col(const float* x, void* out, int N, int C, int T, int H, int W, int KT, int pad_t,
+                                     void* stream) {
+  AVT_REQUIRE(x && out, "video_stem_im2col: null pointer");
+  AVT_REQUIRE(C >= 1 && C <= 4 && KT >= 1 && KT <= 7, "video_stem_im2col: need C <= 4 and KT <= 7");
+  const long long npix = (long long)N * T * H * W;
+  if (npix == 0) return AVT_OK;
+  hipLaunchKernelGGL(video_stem_im2col_kernel, dim3(grid_for(npix)), dim3(256), 0, (hipStream_t)stream, x,
+                     (bf16_t*)out, N, C, T, H * W, KT, pad_t);
+  return check_launch("video_stem_im2col");
+}
+
+// w: fp32 OIDHW [K][C][KT][R][S] -> out bf16 [K][Kg] (fold: stem layout, Kg = R*S*32)
+extern "C" int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, int KT, int R, int S, int fold,
+                                      void* stream) {
+  AVT_REQUIRE(w && out, "pack_conv3d_weight: null pointer");
+  AVT_REQUIRE(!fold || (C <= 4 && KT <= 8), "pack_conv3d_weight: stem fold needs C <= 4, KT <= 8");
+  const long long total = (long long)K * (fold ? R * S * 32 : KT * R * S * C);
+  hipLaunchKernelGGL(pack_conv3d_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)out, K,
+                     C, KT, R, S, fold, total);
+  return check_launch("pack_conv3d_weight");
+}
+
+// Audio de-duplication of the tube step (train_3D.py:128-130 repeats each clip's spectrogram t
+// times): the audio trunk runs once per clip; its unit vector is repeated to the (b t) rows of the
+// head, and the head's gradient is summed back over the t rows (exact: everything between is linear
+// in the upstream gradient for the shared forward).
+extern "C" int avt_repeat_rows_f32(const float* in, float* out, int B, int rep, int C, void* stream) {
+  AVT_REQUIRE(in && out && B >= 0 && rep >= 1 && C >= 1, "repeat_rows_f32: bad arguments");
+  const long long n = (long long)B * rep * C;
+  if (n == 0) return AVT_OK;
+  hipLaunchKernelGGL(repeat_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, B, rep, C);
+  return check_launch("repeat_rows_f32");
+}
+
+extern "C" int avt_sum_rep_rows_f32(const float* in, float* out, int B, int rep, int C, void* stream) {
+  AVT_REQUIRE(in && out && B >= 0 && rep >= 1 && C >= 1, "sum_rep_rows_f32: bad arguments");
+  const long long n = (long long)B * C;
+  if (n == 0) return AVT_OK;
+  hipLaunchKernelGGL(sum_rep_rows_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, in, out, B, rep, C);
+  return check_launch("sum_rep_rows_f32");
+}

@@ -40,16 +40,18 @@ class FlatStore:
     OHWI memory order, exposed as channels_last OIHW ``nn.Parameter`` views, so the kernels read
     them directly and ``state_dict``/``load_state_dict`` keep the reference's key names and shapes."""
 
-    def __init__(self, module: torch.nn.Module):
+    def __init__(self, module: torch.nn.Module, trainable_fn=None):
         self.module = module
+        is_train = trainable_fn if trainable_fn is not None else trainable
+        self.trainable = is_train
         params = [(n, p) for n, p in module.named_parameters()]
-        order = [x for x in params if trainable(x[0])] + [x for x in params if not trainable(x[0])]
+        order = [x for x in params if is_train(x[0])] + [x for x in params if not is_train(x[0])]
         self.pnames = [n for n, _ in order]
         self.n_train = 0
         self.poff: Dict[str, Tuple[int, tuple]] = OrderedDict()
         off = 0
         for n, p in order:
-            if trainable(n):
+            if is_train(n):
                 self.n_train = off + p.numel()
             self.poff[n] = (off, tuple(p.shape))
             off += (p.numel() + 3) // 4 * 4  # 16-byte aligned segments
@@ -128,7 +130,7 @@ class FlatStore:
     def grad_views(self, gflat: torch.Tensor) -> Dict[str, torch.Tensor]:
         out = {}
         for n in self.pnames:
-            if not trainable(n):
+            if not self.trainable(n):
                 continue
             off, shape = self.poff[n]
             k = 1
@@ -169,8 +171,7 @@ class AVEngine:
 
     def __init__(self, flat: FlatStore, epsilon=0.65, epsilon2=0.4, tau=0.03, tri_map=True, neg=True):
         self.flat = flat
-        self.img = Trunk("imgnet.", "vision")
-        self.aud = Trunk("audnet.", "audio")
+        self._setup_trunks()
         self.epsilon, self.epsilon2, self.tau, self.tri_map, self.neg = epsilon, epsilon2, tau, tri_map, neg
         self.store = _EngineStore(self)
         self.packs: Dict[str, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
@@ -180,6 +181,12 @@ class AVEngine:
         self._stat_arena = None
         self._alloc(flat.flat.device)
 
+    def _setup_trunks(self):
+        self.img = Trunk("imgnet.", "vision")
+        self.aud = Trunk("audnet.", "audio")
+        self.trunks2d = [self.img, self.aud]  # packed by the batched 2-D weight pack
+        self.bn_trunks = [self.img, self.aud]  # own fp64 BN accumulators in the arena
+
     def _alloc(self, dev):
         """Persistent device buffers: packed bf16 weights, the batched-pack descriptor table and the
         fp64 BN statistic accumulators (zero between uses)."""
@@ -187,7 +194,7 @@ class AVEngine:
 
         descs = []
         maxel = 0
-        for tr in (self.img, self.aud):
+        for tr in self.trunks2d:
             for spec in tr.convs():
                 wf = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
                 wt = None if spec.is_stem else torch.empty(spec.cin, spec.k * spec.k * spec.cout, device=dev,
@@ -205,7 +212,7 @@ class AVEngine:
         # BN accumulators: per BN 'fwd' [slots][C][3] f64 and 'bwd' [slots][C][2] f64 + k1/k2 (2C f32)
         slots = int(query("avt_bn_slots"))
         offs, total = {}, 0
-        for tr in (self.img, self.aud):
+        for tr in self.bn_trunks:
             for bn in tr.bns():
                 n_f = slots * bn.c * 3
                 n_b = slots * bn.c * 2 + bn.c  # + 2C floats == C doubles

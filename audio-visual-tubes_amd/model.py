@@ -176,3 +176,114 @@ class AVENet(nn.Module):
 
     def _run_layer4_hooks(self):  # test.py:63 registers a forward hook on imgnet.layer4
         raise NotImplementedError("avt: forward hooks on imgnet.layer4 are not supported yet")
+
+
+# ---------------------------------------------------------------------------------------------
+# 3-D tube model (model.py:17-60; BASELINE config 4)
+# ---------------------------------------------------------------------------------------------
+
+
+class HardWayAttention(nn.Module):
+    """model.py:38-60.  Standalone use takes fp32 features (the video map is rounded to bf16 on its
+    way to the head kernel, the precision FullModel's trunk produces it in); inside FullModel the
+    head runs fused on the trunk outputs."""
+
+    def __init__(self):
+        super().__init__()
+        self.sigmoid = nn.Sigmoid()
+        self.epsilon = 0.65
+        self.epsilon2 = 0.4
+        self.tau = 0.03
+
+    def forward(self, audio_features, video_features):
+        from ._lib import call, query
+        from .trunk import P, stream_ptr
+
+        if not video_features.is_cuda or not audio_features.is_cuda:
+            raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
+        b, C, t, h, w = video_features.shape
+        B, Pn = b * t, h * w
+        if tuple(audio_features.shape) != (B, C):
+            raise ValueError(f"avt: audio_features must be [{B},{C}], got {tuple(audio_features.shape)}")
+        dev = video_features.device
+        # '(b t) h w c' bf16 — the FullModel trunk's output layout
+        v = video_features.detach().permute(0, 2, 3, 4, 1).contiguous().to(torch.bfloat16)
+        an = audio_features.detach().float().contiguous()
+        f32 = dict(device=dev, dtype=torch.float32)
+        inv, vsum = torch.empty(B, Pn, **f32), torch.empty(B, Pn, **f32)
+        A0 = torch.empty(B, Pn, B, **f32)
+        save = torch.empty(int(query("avt_hardway_save_floats", B)), **f32)
+        logits = torch.empty(B, B + 2, **f32)
+        A, Pos, Neg = (torch.empty(B, 1, h, w, **f32) for _ in range(3))
+        wA = torch.empty(B, h, w, **f32)
+        call("avt_hardway_fwd", P(v), P(an), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, P(inv), P(vsum),
+             P(A0), P(save), P(logits), P(A), P(Pos), P(Neg), P(wA), stream_ptr())
+        return A, logits
+
+
+class _FullModelFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, training: bool, audio, video, *params):
+        out, tape = engine.forward(audio, video, training)
+        ctx.engine, ctx.tape, ctx.n_params = engine, tape, len(params)
+        ctx.set_materialize_grads(False)
+        return out["A"], out["logits"]
+
+    @staticmethod
+    def backward(ctx, gA, glogits):
+        if gA is not None and bool(torch.any(gA != 0)):
+            raise NotImplementedError("avt: gradients through `A` are not implemented (train_3D.py back-propagates "
+                                      "the logits CE only)")
+        nparams = ctx.n_params
+        if glogits is None:
+            return (None, None, None, None) + (None,) * nparams
+        engine = ctx.engine
+        flat = engine.flat
+        gflat = torch.zeros(flat.n_train, device=glogits.device, dtype=torch.float32)
+        engine.backward(ctx.tape, glogits, gflat)
+        ctx.tape = None
+        views = flat.param_grad_views(gflat)
+        return (None, None, None, None) + tuple(views.get(n) for n in flat.pnames[:nparams])
+
+
+class FullModel(nn.Module):
+    """model.py:17-36 on libavt: R3D-18 ``vidnet`` (forward only; its layer4 is detached as the
+    reference's forward hook does), audio ResNet-18 ``audnet``, AdaptiveMaxPool2d + normalize,
+    HardWayAttention.  ``forward(audio, video) -> (A, logits)`` with audio either the folded
+    repeated spectrogram [b*t,1,F,T] (the reference call, train_3D.py:128-131) or one spectrogram
+    per clip [b,1,F,T] (de-duplicated audio trunk, exact; tube.py)."""
+
+    def __init__(self, args=None):
+        super().__init__()
+        from .resnet3D import generate_model
+
+        self.vidnet = generate_model(model_depth=18, no_max_pool=True, n_classes=1039)
+        self.audnet = resnet18(modal="audio")
+        self.avgpool = nn.AdaptiveMaxPool2d((1, 1))
+        self.attention = HardWayAttention()
+        from .tube import tube_trainable
+
+        self._flat = FlatStore(self, tube_trainable)
+        self._engine = None
+
+    def _apply(self, fn, recurse=True):
+        self._flat.apply(fn)
+        self._engine = None
+        return self
+
+    def engine(self):
+        if self._engine is None:
+            from .tube import TubeEngine
+
+            self._engine = TubeEngine(self._flat)
+        return self._engine
+
+    def forward(self, audio, video):
+        eng = self.engine()
+        named = dict(self.named_parameters())
+        n_train = sum(1 for n in self._flat.pnames if self._flat.trainable(n))
+        train_params = [named[n] for n in self._flat.pnames[:n_train]]
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in train_params):
+            return _FullModelFunction.apply(eng, True, audio, video, *train_params)
+        out, _ = eng.forward(audio, video, self.training)
+        return out["A"], out["logits"]

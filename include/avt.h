@@ -22,6 +22,12 @@
  *                                HardWayAttention.forward (model.py:46-60)
  *   avt_hardway_ce               nn.CrossEntropyLoss()(logits, zeros) (train_hardway_1frame.py:113, 130-131)
  *   avt_adam_step                torch.optim.Adam(lr, weight_decay) step (train_hardway_1frame.py:116, 134)
+ *   avt_conv3d_fwd               nn.Conv3d fwd of the R3D-18 video trunk (models/resnet3D.py:14-28 conv3x3x3 /
+ *                                conv1x1x1, called from BasicBlock.forward 45-61; FullModel.vidnet, model.py:20)
+ *   avt_video_stem_im2col,       the R3D stem Conv3d(3,64,(7,7,7),s(1,2,2),p3) (models/resnet3D.py:122-127) as a
+ *   avt_pack_conv3d_weight       32-channel Conv2d over the frames (temporal taps folded into channels)
+ *   avt_bn_finalize_rep          BatchNorm2d over the t-fold repeated spectrogram batch (train_3D.py:128-130)
+ *                                computed once per distinct clip
  */
 #ifndef AVT_H_
 #define AVT_H_
@@ -78,12 +84,33 @@ size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K,
 int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
                      int S, int stride, int pad, void* workspace, size_t ws_bytes, void* stream);
 
+/* Conv3d, temporal stride 1: y[N,T',P,Q,K] = conv3d(x[N,T,H,W,Cp], wpack[K][(kt,r,s,c)]),
+ * T' = T + 2*pad_t - KT + 1, spatial stride 1 or 2; Cp % 32 == 0; KT*R*S <= 27; bn_acc as conv2d_fwd */
+int avt_conv3d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int T, int H, int W, int Cp,
+                   int K, int KT, int R, int S, int stride, int pad_t, int pad, void* stream);
+/* R3D stem input: x fp32 NCDHW [N][C<=4][T][H][W] -> bf16 [N][T][H][W][32], channel kt*4+c = x[c][t+kt-pad_t]
+ * (zero outside the clip / for c >= C / channels >= 4*KT) */
+int avt_video_stem_im2col(const float* x, void* out, int N, int C, int T, int H, int W, int KT, int pad_t,
+                          void* stream);
+/* w fp32 OIDHW [K][C][KT][R][S] -> bf16 [K][(kt,r,s,c)] (fold 0) or the stem layout
+ * [K][(r,s)][kt*4+c] with 32 channels per (r,s) (fold 1) */
+int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, int KT, int R, int S, int fold, void* stream);
+
+/* tube-step audio de-duplication: out[b*rep+k][:] = in[b][:]  /  out[b][:] = sum_k in[b*rep+k][:] */
+int avt_repeat_rows_f32(const float* in, float* out, int B, int rep, int C, void* stream);
+int avt_sum_rep_rows_f32(const float* in, float* out, int B, int rep, int C, void* stream);
+
 /* ---- batch norm (train mode) ---- */
 /* merge bn_acc (see avt_conv2d_fwd) over `rows` rows -> scale, shift, mean, invstd (fp32 [C]);
  * running stats updated if non-NULL (momentum, unbiased var); bn_acc re-zeroed */
 int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, float* scale, float* shift, float* save_mean,
                     float* save_invstd, void* stream);
+/* avt_bn_finalize for a logical batch in which each accumulated row occurs `rep` times: the running
+ * variance uses the unbiased factor of rows*rep rows (mean/variance are those of the distinct rows) */
+int avt_bn_finalize_rep(double* acc, long long rows, long long rep, int C, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, float momentum, float eps, float* scale,
+                        float* shift, float* save_mean, float* save_invstd, void* stream);
 /* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
 int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                  const float* rshift, void* out, long long rows, int C, int relu, void* stream);
@@ -122,6 +149,7 @@ int avt_hardway_fwd(const void* v, const float* an, int B, int P, int C, float e
                     int use_neg, float* inv, float* vsum, float* A0, float* save, float* logits, float* Aout,
                     float* Pos, float* Neg, float* wA, void* stream);
 int avt_hardway_ce(const float* logits, int B, int L, float scale, float* loss, float* dlogits, void* stream);
+/* dvh = gv = NULL: no vision gradient (detached video features of the tube head) */
 int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
                     const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
                     int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream);

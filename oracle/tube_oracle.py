@@ -174,3 +174,25 @@ def tube_train_step(sd, spec: torch.Tensor, video: torch.Tensor, opt: "orc.AdamR
         with torch.no_grad():
             opt.step({n: sd[n] for n in names}, grads)
     return loss.detach(), A.detach(), logits.detach(), grads
+
+
+def tube_train_step_per_clip(sd, spec: torch.Tensor, video: torch.Tensor):
+    """The de-duplicated form of tube_train_step's forward/backward (what the GPU path runs for a
+    per-clip spectrogram batch): the audio trunk over the b distinct spectrograms, its unit vectors
+    repeated t times into the head.  BN statistics of the repeated batch equal the distinct batch's
+    (the running variance's unbiased factor aside, not exercised here: no Adam, buffers unused).
+    Returns (loss, logits, grads) for the identity test against tube_train_step."""
+    t = video.shape[2]
+    names = trainable_names_tube()
+    leaves = {n: sd[n].detach().clone().requires_grad_(True) for n in names}
+    work = OrderedDict((k, v.clone()) for k, v in sd.items())
+    work.update(leaves)
+    b = spec.shape[0]
+    aud = orc.resnet18_forward(work, "audnet.", spec, "audio", True)
+    aud = F.normalize(F.adaptive_max_pool2d(aud, 1).view(b, -1), dim=1)
+    aud = aud.repeat_interleave(t, dim=0)  # '(b t)' rows, b-major (repeat_spectrogram)
+    vid = F.normalize(r3d18_forward(work, "vidnet.", video, True).detach(), dim=1)
+    A, logits = orc.hardway_attention(aud, vid)
+    loss = orc.hardway_ce(logits)
+    gl = torch.autograd.grad(loss, [leaves[n] for n in names])
+    return loss.detach(), logits.detach(), {n: g for n, g in zip(names, gl)}

@@ -107,3 +107,42 @@ def test_grad_views_layout():
     p = dict(m.named_parameters())
     for n, v in views.items():
         assert v.shape == p[n].shape and v.stride() == p[n].stride(), n
+
+
+# ------------------------------------------------------------------ 3-D tube model (FullModel)
+def test_fullmodel_state_dict_and_trainable_set():
+    import tube_oracle as tor
+    from avt_amd.model import FullModel
+
+    m = FullModel(orc.Args())
+    sd = m.state_dict()
+    ref = tor.fullmodel_entries()
+    assert list(sd.keys()) == [n for n, _, _ in ref]
+    for n, shape, _ in ref:
+        assert tuple(sd[n].shape) == tuple(shape), n
+    names = [n for n in m._flat.pnames if m._flat.trainable(n)]
+    assert sorted(names) == sorted(tor.trainable_names_tube())
+    assert m._flat.n_train == sum(dict(m.named_parameters())[n].numel() for n in names)
+    # vidnet conv weights keep the reference's OIDHW layout (contiguous 5-D views of the flat buffer)
+    assert m.vidnet.conv1.weight.is_contiguous() and m.vidnet.layer1[0].conv1.weight.is_contiguous()
+
+
+def test_fullmodel_torch_seeded_init_matches_reference(golden_dir):
+    from avt_amd.model import FullModel
+
+    g = dict(np.load(os.path.join(golden_dir, "fullmodel_torch_init_seed0.npz"), allow_pickle=False))
+    torch.manual_seed(0)
+    m = FullModel(orc.Args())
+    sd = m.state_dict()
+    assert list(sd.keys()) == [str(k) for k in g["keys"]]
+    for n, cs in zip(g["names"], g["checksums"]):
+        np.testing.assert_allclose(checksum(sd[str(n)]), cs, rtol=1e-10, atol=1e-10, err_msg=str(n))
+
+
+def test_fullmodel_refuses_cpu():
+    import tube_oracle as tor
+    from avt_amd.model import FullModel
+
+    m = FullModel(orc.Args())
+    with pytest.raises(RuntimeError):
+        m(orc.make_spectrogram(1, 65, 76), tor.make_video(1, 2, 32))

@@ -74,3 +74,19 @@ def test_tube_oracle_fp32_tolerance(golden_dir):
     np.testing.assert_allclose(A.numpy(), g["A_f64"], atol=1e-5)
     off = ~np.eye(logits.shape[0], logits.shape[1], k=1, dtype=bool)
     np.testing.assert_allclose(logits.numpy()[off], g["logits_f64"][off], atol=1e-3)
+
+
+def test_per_clip_audio_is_exact_in_fp64(golden_dir):
+    """Running the audio trunk once per clip and repeating its unit vector over the clip's t frames
+    gives the folded repeated batch's loss and gradients exactly (fp64): the identity the GPU path's
+    per-clip mode (tube.py, avt_repeat_rows_f32 / avt_sum_rep_rows_f32 / avt_bn_finalize_rep) uses."""
+    g = _load(golden_dir, "fullmodel_tiny_b2t4")
+    video, spec = _inputs(g)
+    sd = tor.make_tube_state(0, torch.float64)
+    sd_a = {k: v.clone() for k, v in sd.items()}
+    loss, _, logits, grads = tor.tube_train_step(sd_a, spec.double(), video.double(), None)
+    loss2, logits2, grads2 = tor.tube_train_step_per_clip(sd, spec.double(), video.double())
+    assert abs(loss.item() - loss2.item()) < 1e-12
+    torch.testing.assert_close(logits2, logits, rtol=1e-12, atol=1e-12)
+    for n in grads:
+        torch.testing.assert_close(grads2[n], grads[n], rtol=1e-9, atol=1e-14)
