@@ -1,18 +1,26 @@
-"""Train-step clips/s of the 1-frame audio-visual hard-way step (BASELINE.json metric) on MI355X.
+"""Train-step clips/s of the audio-visual hard-way step (BASELINE.json metric) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload 1frame|tube]
+                    [--no-cpu-baseline]
     (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
-Workload (BASELINE.json configs[1]): per GPU B=128 clips of one 224x224 RGB frame + one 257x300
-log-spectrogram; ResNet-18 vision + ResNet-18 audio trunks (bf16 MFMA, fp32 statistics), fp32
-hard-way head + CE, backward, Adam (lr 1e-6, wd 1e-4); N GPUs = weak scaling with local
-negatives and one RCCL all-reduce of the 89.4 MB fp32 gradient per step.  Inputs are synthetic
-and already resident in HBM when the timed region starts; weights are random-init (no checkpoints).
+Default workload (BASELINE.json configs[1], the headline): per GPU B=128 clips of one 224x224 RGB
+frame + one 257x300 log-spectrogram; ResNet-18 vision + ResNet-18 audio trunks (bf16 MFMA, fp32
+statistics), fp32 hard-way head + CE, backward, Adam (lr 1e-6, wd 1e-4); N GPUs = weak scaling with
+local negatives and one RCCL all-reduce of the 89.4 MB fp32 gradient per step.
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel family (the implicit-GEMM
-convolutions: fwd + dgrad + wgrad), measured live with HIP events around every conv launch inside
-the timed steps: achieved = algorithmic conv FLOPs / summed kernel time.  `cpu_baseline` times the
-oracle's fp32 PyTorch-CPU restatement of the same step (B=2) on the host cores (rank 0, N=1 only).
+--workload tube (configs[3], train_3D.py): per GPU b=8 clips of 16x224x224 frames + one 257x300
+spectrogram each; R3D-18 forward (detached, as the reference's hook) + audio ResNet-18 fwd/bwd over
+the 16-fold repeated spectrogram (run once per clip unless --tube-folded: exact, tube.py) + the
+hard-way head over the (b t) = 128 rows + CE + Adam.
+
+Inputs are synthetic and already resident in HBM when the timed region starts; weights are
+random-init (no checkpoints).  Prints ONE JSON line on rank 0.  `roofline` is for the dominant
+kernel family (the implicit-GEMM convolutions), measured live with HIP events around every conv
+launch of eager steps run right after the timed region: achieved = algorithmic conv FLOPs / summed
+kernel time; `traffic` = PMC-measured HBM bytes per conv launch from the committed profile of the
+same workload (tools/pmc_traffic.sh).  `cpu_baseline` times the oracle's fp32 PyTorch-CPU
+restatement of the same step on the host cores (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -28,63 +36,87 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-GFLOP_PER_CLIP = 46.87  # fwd 15.74 + bwd 31.12 (torch.utils.flop_counter on the reference)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
 
+METRIC = "train-step clips/sec (whole node), ResNet18+VGG-M hard-way loss at 1/2/4/8 GPU"
+DATA = "synthetic (seeded N(0,1) frames, clipped N(-1.16,0.08^2) log-spectrograms; random-init weights)"
 
-def synthetic_inputs(B, device, seed):
+
+def synthetic_inputs(B, device, seed, frames=0):
     g = torch.Generator(device=device).manual_seed(seed)
-    img = torch.randn(B, 3, 224, 224, device=device, generator=g)
+    if frames:
+        img = torch.randn(B, 3, frames, 224, 224, device=device, generator=g)
+    else:
+        img = torch.randn(B, 3, 224, 224, device=device, generator=g)
     spec = (torch.randn(B, 1, 257, 300, device=device, generator=g) * 0.08 - 1.16).clamp_(-1.35, -0.6)
     return img, spec
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "conv_traffic_b128.json")
+def traffic_file(workload, B):
+    return os.path.join(REPO, "profiles", f"conv_traffic_{'b' if workload == '1frame' else 'tube_b'}{B}.json")
 
 
-def conv_traffic(launches_per_step, B, world):
+def conv_traffic(path, launches_per_step, B):
     """HBM bytes per conv launch from the committed PMC summary (tools/pmc_traffic.sh ->
     tools/traffic_summary.py --json) of this same workload; None if absent or for another batch."""
     try:
-        with open(TRAFFIC_FILE) as f:
+        with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None, None
     if t.get("per_gpu_batch") != B or launches_per_step <= 0:
         return None, None
     per_step = t["conv_read_bytes_per_step"] + t["conv_write_bytes_per_step"]
-    return round(per_step / launches_per_step), os.path.relpath(TRAFFIC_FILE, REPO)
+    return round(per_step / launches_per_step), os.path.relpath(path, REPO)
 
 
-def cpu_baseline(budget_s: float = 20.0):
-    """Oracle (fp32 PyTorch CPU restatement) full train step at B=2 on the host cores."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import avenet_oracle as orc
-
+def _cores():
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
-    torch.set_num_threads(cores)
-    B = 2
-    sd = orc.make_state(0)
-    img, aud = orc.make_image(B), orc.make_spectrogram(B)
-    opt = orc.AdamRef()
-    orc.train_step(sd, img, aud, opt)  # warm-up
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+
+
+def _time_loop(fn, budget_s, max_n=50):
+    fn()  # warm-up
     times = []
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or len(times) < 3:
         t0 = time.perf_counter()
-        orc.train_step(sd, img, aud, opt)
+        fn()
         times.append(time.perf_counter() - t0)
-        if len(times) >= 50:
+        if len(times) >= max_n:
             break
     times.sort()
-    med = times[len(times) // 2]
+    return times[len(times) // 2], len(times)
+
+
+def cpu_baseline(workload: str, budget_s: float = 20.0):
+    """The oracle (fp32 PyTorch-CPU restatement) of the same step on the host cores."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import avenet_oracle as orc
+
+    cores = _cores()
+    torch.set_num_threads(cores)
+    if workload == "tube":
+        import tube_oracle as tor
+
+        sd = tor.make_tube_state(0)
+        video, spec = tor.make_video(1, 16, 224), orc.make_spectrogram(1)
+        opt = orc.AdamRef()
+        med, n = _time_loop(lambda: tor.tube_train_step(sd, spec, video, opt), budget_s, max_n=10)
+        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port",
+                "sample": f"oracle fp32 train_3D step (R3D-18 fwd + 16x-repeated audio ResNet-18 fwd/bwd + head + "
+                          f"Adam), b=1 clip of 16x224^2 + 257x300, median of {n}"}
+    B = 2
+    sd = orc.make_state(0)
+    img, aud = orc.make_image(B), orc.make_spectrogram(B)
+    opt = orc.AdamRef()
+    med, n = _time_loop(lambda: orc.train_step(sd, img, aud, opt), budget_s)
     return {"value": B / med, "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"oracle fp32 full train step (fwd+CE+bwd+Adam), B=2, 224^2 + 257x300, median of {len(times)}"}
+            "sample": f"oracle fp32 full train step (fwd+CE+bwd+Adam), B=2, 224^2 + 257x300, median of {n}"}
 
 
 def main():
@@ -92,7 +124,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=128, help="clips per GPU")
+    ap.add_argument("--workload", choices=["1frame", "tube"], default="1frame")
+    ap.add_argument("--batch", type=int, default=0, help="clips per GPU (default 128; tube: 8)")
+    ap.add_argument("--frames", type=int, default=16, help="tube: frames per clip")
+    ap.add_argument("--tube-folded", action="store_true", help="tube: run the audio trunk over the folded "
+                    "16x-repeated spectrogram batch (the reference's arithmetic) instead of once per clip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel eagerly instead of replaying a "
@@ -110,31 +146,44 @@ def main():
     dev = torch.device("cuda", local)
 
     import avtubes  # noqa: F401
-    from avt_amd.model import AVENet
+    from avt_amd.model import AVENet, FullModel
     from avt_amd.train import HardWayTrainStep
     from avt_amd.trunk import ConvProfiler
 
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import avenet_oracle as orc
 
+    tube = args.workload == "tube"
+    B = args.batch or (8 if tube else 128)
     torch.manual_seed(0)
-    model = AVENet(orc.Args(), False).to(dev).train()
+    if tube:
+        model = FullModel(orc.Args()).to(dev).train()
+        video, spec = synthetic_inputs(B, dev, seed=1000 + rank, frames=args.frames)
+        if args.tube_folded:  # train_3D.py:128-130
+            spec = spec.unsqueeze(2).repeat(1, 1, args.frames, 1, 1).transpose(1, 2).reshape(
+                B * args.frames, 1, 257, 300).contiguous()
+        x1, x2 = spec, video
+        workload = (f"train_3D step: b={B} clips of {args.frames}x224x224 frames + 257x300 spectrogram, R3D-18 fwd "
+                    f"+ audio ResNet-18 fwd/bwd ({'folded (b t) batch' if args.tube_folded else 'once per clip'}) "
+                    f"+ hard-way head over (b t)={B * args.frames} rows + CE + Adam")
+    else:
+        model = AVENet(orc.Args(), False).to(dev).train()
+        x1, x2 = synthetic_inputs(B, dev, seed=1000 + rank)
+        workload = "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam"
     step = HardWayTrainStep(model, lr=1e-6, weight_decay=1e-4)
-    B = args.batch
-    img, aud = synthetic_inputs(B, dev, seed=1000 + rank)
 
     use_graph = not args.no_graph
     for i in range(max(args.warmup, 1 if use_graph else 0)):
-        loss = step.step(img, aud)
+        loss = step.step(x1, x2)
         if use_graph and i == 0:
-            step.capture(img, aud)  # later warm-up and all timed steps are graph replays
+            step.capture(x1, x2)  # later warm-up and all timed steps are graph replays
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step.step(img, aud)
+        loss = step.step(x1, x2)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -148,7 +197,7 @@ def main():
     eager._graph = None
     with ConvProfiler() as prof:
         for _ in range(args.prof_steps):
-            eager.step(img, aud)
+            eager.step(x1, x2)
         torch.cuda.synchronize()
     conv = prof.summary()
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -156,29 +205,32 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = el.item()
     if rank == 0:
+        ps = max(args.prof_steps, 1)
         clips = B * world * args.steps
         value = clips / elapsed
+        ms_step = elapsed / args.steps * 1e3
         fl = sum(v[1] for v in conv.values())
         ms = sum(v[2] for v in conv.values())
         n_launch = sum(v[0] for v in conv.values())
         alg_bytes = sum(v[3] for v in conv.values())
         achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-        traffic, traffic_src = conv_traffic(n_launch / max(args.prof_steps, 1), B, world)
+        traffic, traffic_src = conv_traffic(traffic_file(args.workload, B), n_launch / ps, B)
+        conv_tflop_step = fl / ps / 1e12
         rec = {
-            "metric": "train-step clips/sec (whole node), ResNet18 vision + ResNet18 audio hard-way loss",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "clips/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (seeded N(0,1) frames, clipped N(-1.16,0.08^2) log-spectrograms; random-init weights)",
-            "config": {"workload": "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam",
-                       "global_batch": B * world, "per_gpu_batch": B, "parallelism": f"dp{world}"},
+            "data": DATA,
+            "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B,
+                       "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM (fwd+dgrad+wgrad)",
                          "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
@@ -188,18 +240,20 @@ def main():
                          "algorithmic_flops_per_launch": round(fl / max(n_launch, 1)),
                          "launches": n_launch,
                          "per_kind": {k: {"launches": v[0], "tflops": round(v[1] / (v[2] * 1e-3) / 1e12, 2),
-                                          "ms_per_step": round(v[2] / max(args.prof_steps, 1), 3)} for k, v in conv.items()},
-                         "conv_ms_per_step": round(ms / max(args.prof_steps, 1), 3),
+                                          "ms_per_step": round(v[2] / ps, 3)} for k, v in conv.items()},
+                         "conv_ms_per_step": round(ms / ps, 3),
                          "measured": f"HIP events around each conv launch, {args.prof_steps} eager steps after the "
                                      "timed region"},
             "launch": "eager" if args.no_graph else "hip-graph replay",
-            "step_tflops_per_gpu": round(value / world * GFLOP_PER_CLIP / 1e3, 2),
-            "step_mfma_frac": round(value / world * GFLOP_PER_CLIP / 1e3 / MFMA_BF16_PEAK_TFLOPS, 4),
+            # whole step: algorithmic conv FLOPs of one step / step time (head, BN, Adam: < 1 %)
+            "step_conv_tflop": round(conv_tflop_step, 4),
+            "step_tflops_per_gpu": round(conv_tflop_step / (ms_step * 1e-3), 2),
+            "step_mfma_frac": round(conv_tflop_step / (ms_step * 1e-3) / MFMA_BF16_PEAK_TFLOPS, 4),
             "loss": round(loss_v, 6),
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+            rec["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_budget)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()
