@@ -34,6 +34,13 @@ def trainable(name: str) -> bool:
     return True
 
 
+def _numel(shape) -> int:
+    n = 1
+    for s in shape:
+        n *= s
+    return n
+
+
 class FlatStore:
     """All parameters of a module in one flat fp32 buffer (trainable ones first), all float
     buffers in a second one, num_batches_tracked counters in a third.  Conv weights are kept in
@@ -288,8 +295,32 @@ class AVEngine:
         return out, tape
 
     # ----------------------------------------------------------------------------- backward
-    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor):
-        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it)."""
+    def grad_buckets(self):
+        """Gradient all-reduce buckets in backward completion order, as (boundary tag, flat region):
+        each trunk's layer3+layer4 ('<prefix>hi'), then the rest of it ('<prefix>lo').  backward()
+        calls on_boundary(tag) when a bucket's gradients are final."""
+        order = [tr for tr in self.backward_order()]
+        out = []
+        for tr in order:
+            hi = lambda n, p=tr.prefix: n.startswith(p + "layer3.") or n.startswith(p + "layer4.")
+            lo = lambda n, p=tr.prefix: n.startswith(p) and not (n.startswith(p + "layer3.") or
+                                                                 n.startswith(p + "layer4."))
+            for tag, sel in ((tr.prefix + "hi", hi), (tr.prefix + "lo", lo)):
+                spans = [(self.flat.poff[n][0], self.flat.poff[n][0] + _numel(self.flat.poff[n][1]))
+                         for n in self.flat.pnames if self.flat.trainable(n) and sel(n)]
+                lo_off, hi_off = min(a for a, _ in spans), max(b for _, b in spans)
+                # the region is exactly these parameters' grads (+ 16-byte alignment padding)
+                assert sum(b - a for a, b in spans) <= hi_off - lo_off <= sum(b - a for a, b in spans) + 3 * len(spans)
+                hi_off = min((hi_off + 3) // 4 * 4, self.flat.n_train)
+                out.append((tag, (lo_off, hi_off)))
+        return out
+
+    def backward_order(self):
+        return [self.img, self.aud]
+
+    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor, on_boundary=None):
+        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).  on_boundary(tag)
+        is called as each grad_buckets() bucket becomes final (for an overlapped all-reduce)."""
         B, Pn, C = tape["B"], tape["P"], tape["C"]
         dev = dlogits.device
         f32 = dict(device=dev, dtype=torch.float32)
@@ -307,7 +338,11 @@ class AVEngine:
              a.shape[1] * a.shape[2], C, stream_ptr())
         self.store.grads = self.flat.grad_views(gflat)
         try:
-            self.img.backward(tape["img"], gv, self.store)
-            self.aud.backward(tape["aud"], ga, self.store)
+            self.img.backward(tape["img"], gv, self.store, on_boundary)
+            if on_boundary is not None:
+                on_boundary(self.img.prefix + "lo")
+            self.aud.backward(tape["aud"], ga, self.store, on_boundary)
+            if on_boundary is not None:
+                on_boundary(self.aud.prefix + "lo")
         finally:
             self.store.grads = None

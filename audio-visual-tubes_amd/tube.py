@@ -262,7 +262,10 @@ class TubeEngine(AVEngine):
         return out, tape
 
     # ----------------------------------------------------------------------------- backward
-    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor):
+    def backward_order(self):
+        return [self.aud]
+
+    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor, on_boundary=None):
         """Accumulate d(loss)/d(audnet params) into gflat[:n_train] (caller zeroes it)."""
         B, Pn, C, rep, Ba = tape["B"], tape["P"], tape["C"], tape["rep"], tape["Ba"]
         dev = dlogits.device
@@ -284,6 +287,8 @@ class TubeEngine(AVEngine):
              a.shape[1] * a.shape[2], C, stream_ptr())
         self.store.grads = self.flat.grad_views(gflat)
         try:
-            self.aud.backward(tape["aud"], ga, self.store)
+            self.aud.backward(tape["aud"], ga, self.store, on_boundary)
+            if on_boundary is not None:
+                on_boundary(self.aud.prefix + "lo")
         finally:
             self.store.grads = None

@@ -1,0 +1,121 @@
+"""Data-parallel train step on the GPU, two ranks sharing the box's one GPU over the gloo backend
+(RCCL needs one device per rank; the step's collective calls are backend-agnostic).
+
+Each rank runs HardWayTrainStep on its half of the batch with the bucketed, backward-overlapped
+gradient all-reduce (train.py), eager and then as captured segment graphs.  The parameters must
+follow the single-process data-parallel update: Adam on the mean of the two local-negative
+gradients (nn.DataParallel semantics, train_hardway_1frame.py:93; model.py:114-115)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import avenet_oracle as orc
+
+pytestmark = pytest.mark.gpu
+B_LOCAL, S, F, T = 2, 64, 65, 76
+STEPS_EAGER, STEPS_GRAPH = 2, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shards():
+    img = orc.make_image(2 * B_LOCAL, S)
+    aud = orc.make_spectrogram(2 * B_LOCAL, F, T)
+    return [(img[r * B_LOCAL:(r + 1) * B_LOCAL], aud[r * B_LOCAL:(r + 1) * B_LOCAL]) for r in range(2)]
+
+
+def _model(dev):
+    import avtubes  # noqa: F401
+    from avt_amd.model import AVENet
+
+    m = AVENet(orc.Args(), False)
+    m.load_state_dict(orc.make_state(0))
+    return m.to(dev).train()
+
+
+def _worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import avtubes  # noqa: F401  (registers avt_amd in this spawned interpreter)
+        from avt_amd.train import HardWayTrainStep
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        m = _model(dev)
+        step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
+        img, aud = (t.to(dev) for t in _shards()[rank])
+        losses = [step.step(img, aud).item() for _ in range(STEPS_EAGER)]
+        step.capture(img.clone(), aud.clone())
+        losses += [step.step(img, aud).item() for _ in range(STEPS_GRAPH)]
+        torch.cuda.synchronize()
+        out_q.put((rank, np.array(losses), m._flat.flat.cpu().numpy().copy(), len(step._seg_graphs)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_bucketed_allreduce_matches_dp_mean():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    import queue
+    import time
+
+    t_end = time.time() + 150
+    while len(res) < world:
+        try:
+            r, losses, flat, nseg = q.get(timeout=5)
+            res[r] = (losses, flat, nseg)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() > t_end:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"rank process failed (exit codes {[p.exitcode for p in procs]})")
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][2] == 4  # imgnet hi/lo, audnet hi/lo segment graphs
+    # both ranks hold the same weights
+    assert np.abs(res[0][1] - res[1][1]).max() == 0.0
+
+    # single-process reference: Adam on the mean of the two shards' gradients
+    import avtubes  # noqa: F401
+    from avt_amd.train import HardWayTrainStep
+
+    dev = torch.device("cuda", 0)
+    m = _model(dev)
+    ref = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
+    shards = [(a.to(dev), b.to(dev)) for a, b in _shards()]
+    ref_losses = [[], []]
+    for _ in range(STEPS_EAGER + STEPS_GRAPH):
+        gsum = torch.zeros_like(ref.grad)
+        for r, (img, aud) in enumerate(shards):
+            ref_losses[r].append(ref._fwd_bwd(img, aud).item())
+            gsum += ref.grad
+        ref.opt.step(gsum, grad_scale=0.5)
+    torch.cuda.synchronize()
+    for r in range(world):
+        np.testing.assert_allclose(res[r][0], ref_losses[r], rtol=1e-4)
+    d = np.abs(res[0][1] - m._flat.flat.cpu().numpy()).max()
+    print(f"max |param(2 ranks) - param(DP reference)| = {d:.3e}")
+    # each Adam step moves a weight by <= ~lr; split-K atomics may flip a ~0 gradient's update
+    assert d <= (STEPS_EAGER + STEPS_GRAPH) * 2.1e-6, d
