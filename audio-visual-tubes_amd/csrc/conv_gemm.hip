@@ -458,6 +458,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 
 #include "conv_nt_pipe.h"
 #include "conv_tn_pipe.h"
+#include "conv_halo.h"
 
 static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
 static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
@@ -477,6 +478,14 @@ static int num_cus() {
   }
   return n;
 }
+static int g_halo = -1;  // 3x3/s1 fwd/dgrad on the halo-reuse kernel: -1 = env AVT_HALO (default 1)
+static int halo_enabled() {
+  if (g_halo < 0) {
+    const char* e = getenv("AVT_HALO");
+    g_halo = e ? atoi(e) : 1;
+  }
+  return g_halo;
+}
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -492,6 +501,11 @@ using namespace avt;
 
 extern "C" int avt_set_conv_variant(int v) {
   avt::g_conv_variant = v;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_halo(int on) {
+  avt::g_halo = on < 0 ? 0 : (on > 2 ? 2 : on);
   return AVT_OK;
 }
 
@@ -599,8 +613,56 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
     }
 }
 
+constexpr int kHaloPR = 416;  // patch rows the halo kernels' LDS holds: 256 + 2W + 2 <= 416 -> W <= 79
+
+// 3x3 / stride 1 / pad 1 Conv2d, 64-channel multiples, image width <= 79: the halo-reuse kernel
+static bool halo_eligible(const GemmNTParams& p) {
+  const int h = halo_enabled();
+  if (!h || p.R != 3 || p.S != 3 || p.stride != 1 || p.pad != 1 || p.IC % 64 != 0 || p.IT > 1 || p.OT > 1 ||
+      p.IH != p.OH || p.IW != p.OW)
+    return false;
+  if (h == 2) return 256 + 2 * p.OW + 2 <= kHaloPR && (p.Ng % 128 == 0 || p.Ng == 64);  // 8-wave forms (A/B)
+  return p.Ng % 128 == 0 && 128 + 2 * p.OW + 2 <= 168;                                // W <= 19
+}
+
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR>
+static void launch_halo(const GemmNTParams& p, hipStream_t st) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  HaloArgs ha{};
+  const int batch = p.M / (p.OH * p.OW);
+  ha.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * p.IC * 2);
+  ha.w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
+  ha.W = p.OW;
+  ha.H = p.OH;
+  for (int r = 0; r < 3; ++r)
+    for (int s = 0; s < 3; ++s) {
+      const int t = r * 3 + s;
+      const int dy = MODE == MODE_FWD ? r - 1 : 1 - r, dx = MODE == MODE_FWD ? s - 1 : 1 - s;
+      ha.tap_dy[t] = dy;
+      ha.tap_dx[t] = dx;
+      ha.tap_disp[t] = dy * p.OW + dx;
+      ha.tap_w[t] = t;
+    }
+  const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
+  if (grid > 0)
+    hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX>), dim3(grid), dim3(WM * WN * 64), 0, st,
+                       p, ha);
+}
+
 template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
+  if (CVEC == 8 && conv_variant() == 1 && halo_eligible(p)) {
+    // measured (tools/conv_bench.py): the 4-wave 128 x 128 form at 2 blocks per CU beats the tap
+    // gather on layer3/4 (W <= 19: +2..16 %); the 8-wave 256-row forms a patch of the wider layer1/2
+    // images needs (1 block per CU) lose to it (-1..-20 %), so those keep the tap-gather kernel
+    if (g_halo == 2 && p.Ng % 128 == 0)
+      launch_halo<MODE, 4, 2, 2, 2>(p, st);  // 256 x 128, 8 waves (A/B only)
+    else if (g_halo == 2)
+      launch_halo<MODE, 4, 2, 2, 1>(p, st);  // 256 x 64, 8 waves (A/B only)
+    else
+      launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st);  // 128 x 128, 4 waves, 77 KB LDS: 2 blocks per CU
+    return;
+  }
   if (CVEC == 8 && conv_variant() == 1) {
     if (p.Ng % 128 == 0) {
       // default: 256-row tiles (8 waves) where the GEMM is tall enough to fill the chip with them

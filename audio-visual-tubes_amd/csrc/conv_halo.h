@@ -1,0 +1,294 @@
+// Halo-reuse implicit-GEMM 3x3 / stride-1 / pad-1 convolution (fwd and dgrad), NHWC bf16, MFMA.
+// Included by conv_gemm.hip inside namespace avt (after conv_nt_pipe.h: wait_vmcnt, xcd_remap,
+// buf_lds16, swz_rb, kOOB, GemmNTParams, MODE_*).
+//
+// For a 3x3 stride-1 "same" conv the output grid equals the input grid, so output pixel m reads
+// input pixel m + (dy*W + dx) for its 9 taps (dy, dx in -1..1; image borders masked).  A tile of BM
+// consecutive output pixels [m0, m0+BM) therefore reads only the contiguous input range
+// [m0 - W - 1, m0 + BM + W + 1): its "patch".  The tap-gather kernel (conv_nt_pipe_kernel) moves
+// every input row through L2 -> LDS once per tap (9x); this kernel moves the patch once per 64-channel
+// chunk and reads the 9 tap-shifted windows out of LDS, so the activation fill per chunk drops from
+// 9*BM rows to BM + 2W + 2 rows (1.2-1.9x BM at the trunk shapes).  The k loop walks (chunk, tap),
+// tap fastest: per step one weight tile [BN x 64] streams through an NSTB-stage ring, and 1/9 of
+// the NEXT chunk's patch streams into the other half of a double-buffered patch (pieces issued only
+// once the step reading the previous chunk's last tap has passed, so the buffer is free).
+// Masked taps (image border, m >= M) read a zero row.  Dgrad (stride 1) is the same loop over dy
+// with the flipped taps and the [C][(r,s,k)] weight operand.
+#pragma once
+
+struct HaloArgs {
+  unsigned act_bytes, w_bytes;
+  int W, H;              // image (= output) width / height
+  int tap_disp[9];       // input-pixel displacement dy*W + dx of each tap
+  int tap_dy[9], tap_dx[9];
+  int tap_w[9];          // weight tap index of each listed tap
+};
+
+// WM x WN waves, each TM x TN 32x32 accumulators: BM = WM*TM*32 rows, BN = WN*TN*32 columns.
+// NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX>
+__global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p, HaloArgs ha) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int BK = 64, RB = 128, RPI = 8;  // 64 channels = one 128-B row; 8 rows per 1 KiB DMA
+  constexpr int BR = BN / (NW * RPI);        // weight-tile DMA instructions per wave per step
+  static_assert(BR >= 1 && BR * NW * RPI == BN, "weight tile / wave split");
+  constexpr int PINSTR = (PRMAX + RPI - 1) / RPI;  // DMA instructions per patch
+  static_assert(NSTB == 2 || NSTB == 3, "NSTB");
+  constexpr int NPIECE = 10 - NSTB;  // patch pieces ride on taps NSTB-1 .. 8
+  constexpr int AP = (PINSTR + NPIECE * NW - 1) / (NPIECE * NW);  // patch instructions per wave per piece
+  constexpr int ABUF = PRMAX * RB;
+  constexpr int BSTAGE = BN * RB;
+  constexpr int CT_LD = BN + 8;
+  constexpr int EPI_BYTES = BM * CT_LD * 2;
+  constexpr int MAIN = 2 * ABUF + NSTB * BSTAGE;
+  constexpr int SMEM = (MAIN > EPI_BYTES ? MAIN : EPI_BYTES);
+  static_assert(PRMAX % RPI == 0, "PRMAX");
+  // + 1 KiB of zeros: the row masked taps read, and the sink of the constant-count dummy DMAs
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 1024 + 2 * WM * BN * 4];
+  char* zrow = smem + SMEM;
+  float* red = reinterpret_cast<float*>(smem + SMEM + 1024);  // [2][WM][BN] epilogue scratch
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int nnt = p.Ng / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / nnt, nt = bid - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int W = ha.W, H = ha.H, hw = W * H;
+  const int pre = W + 1;  // patch row of output pixel m0 is pre
+  const int PR = BM + 2 * pre;
+  const int nchunk = p.IC / BK;
+  const int S = nchunk * 9;
+
+  if (tid < 64) reinterpret_cast<u32x4*>(zrow)[tid] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)ha.act_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.wmat, (short)0, (int)ha.w_bytes, 0x00020000);
+
+  // ---- DMA lane geometry: lane -> (row within the 8-row instruction, 16-B chunk) ----
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  // patch instruction q (of PINSTR) covers patch rows 8q..8q+7; row pr = 8q + lrow holds input pixel
+  // m0 - pre + pr, its chunk (pchunk ^ swz) stored at lane position pchunk (source-side swizzle)
+  auto patch_voff = [&](int q, int chunk_c) -> unsigned {
+    const int pr = q * RPI + lrow;
+    const int pix = m0 - pre + pr;
+    if (q >= PINSTR || pr >= PR || pix < 0 || pix >= p.M) return kOOB;
+    const int lc = pchunk ^ ((pr >> 1) & 7);
+    return (unsigned)(((long long)pix * p.IC + chunk_c * BK + lc * 8) * 2);
+  };
+  unsigned b_off[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int row = (wid * BR + i) * RPI + lrow;
+    const int lc = pchunk ^ ((row >> 1) & 7);
+    b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
+  }
+  // tap table in VGPR lanes (read with v_readlane: no scalar-memory wait in the loop)
+  int lane_tapw = 0, lane_disp = 0;
+  if (lane < 9) {
+    lane_tapw = ha.tap_w[lane] * p.IC * 2;
+    lane_disp = ha.tap_disp[lane];
+  }
+
+  // ---- fragment rows of this lane: rows wm*(BM/WM) + i*32 + (lane & 31); per row a 9-bit tap mask ----
+  const int frow = lane & 31, fhalf = lane >> 5;
+  unsigned fmask[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int row = wm * (BM / WM) + i * 32 + frow;
+    const int m = m0 + row;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    const int n = mm / hw, rem = mm - n * hw;
+    const int oh = rem / W, ow = rem - oh * W;
+    unsigned mk = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int y = oh + ha.tap_dy[t], x = ow + ha.tap_dx[t];
+      mk |= (ok && y >= 0 && y < H && x >= 0 && x < W ? 1u : 0u) << t;
+    }
+    fmask[i] = mk;
+  }
+
+  // ---- issue of step j: weight tile (tap t, chunk c) into ring stage j % NSTB, and for t >= 2 one
+  //      piece of chunk c+1's patch into patch buffer (c+1) & 1 ----
+  int is_c = 0, is_t = 0;  // (chunk, tap) of the next step to issue (wave-uniform)
+  auto issue = [&](int j) {
+    char* Bs = smem + 2 * ABUF + (j % NSTB) * BSTAGE;
+    const bool live = j < S;
+    const int t = live ? is_t : 0;
+    const unsigned boff = (unsigned)(__builtin_amdgcn_readlane(lane_tapw, t) + is_c * BK * 2);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
+    if (is_t >= NSTB - 1) {  // the buffer (c+1)&1 held chunk c-1, whose last reader has passed
+      char* Ab = smem + ((is_c + 1) & 1) * ABUF;
+      const bool alive = live && is_c + 1 < nchunk;
+#pragma unroll
+      for (int a = 0; a < AP; ++a) {
+        const int q = ((is_t - (NSTB - 1)) * AP + a) * NW + wid;  // pieces 0..6 of the patch
+        const bool inrange = q < PINSTR;
+        // out-of-range instructions still issue (constant vmcnt): zeros into the zero area
+        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, is_c + 1) : kOOB);
+      }
+    }
+    if (++is_t == 9) {
+      is_t = 0;
+      ++is_c;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2
+  for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, 0));
+#pragma unroll
+  for (int j = 0; j < NSTB - 1; ++j) issue(j);
+
+  constexpr int KS = BK / 16;
+  bf16x8 af[2][TM], bfr[2][TN];
+  int rowaddr[TM], rowsw[TM];
+  for (int s = 0; s < S; ++s) {
+    const int c = s / 9, t = s - c * 9;
+    // step s has landed once only step s+1's loads may be outstanding (issued after it)
+    if constexpr (NSTB == 2) {
+      wait_vmcnt<0>();
+    } else {
+      const int tn = t + 1 == 9 ? 0 : t + 1;
+      if (tn >= NSTB - 1)
+        wait_vmcnt<BR + AP>();
+      else
+        wait_vmcnt<BR>();
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* Ab = smem + (c & 1) * ABUF;
+    const char* Bs = smem + 2 * ABUF + (s % NSTB) * BSTAGE;
+    const int disp = __builtin_amdgcn_readlane(lane_disp, t);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int pr = wm * (BM / WM) + i * 32 + frow + pre + disp;
+      const bool v = (fmask[i] >> t) & 1u;
+      // masked taps read zeros from the zero area, at the bank position the real row would have
+      rowaddr[i] = (v ? (int)(Ab - smem) : SMEM - (pr & ~7) * RB) + pr * RB;
+      rowsw[i] = (pr >> 1) & 7;
+    }
+    auto load_frags = [&](int ks, int buf) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[buf][i] = *reinterpret_cast<const bf16x8*>(smem + rowaddr[i] + (((ks * 2 + fhalf) ^ rowsw[i]) << 4));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * (BN / WN) + j * 32 + frow;
+        bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + swz_rb<RB>(row, ks * 2 + fhalf));
+      }
+    };
+    load_frags(0, 0);
+    issue(s + NSTB - 1);  // the ring stage read at step s-1; every wave has passed that
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+        load_frags(ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+      if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  // ---- epilogue (as conv_nt_pipe_kernel): BN partial statistics, bf16 tile through LDS, (+ add) ----
+  const int rows_valid = min(BM, p.M - m0);
+  if (MODE == MODE_FWD && p.stats != nullptr) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          if (r < rows_valid) sm += acc[i][j][v];
+        }
+      sm += __shfl_xor(sm, 32, 64);
+      if (lane < 32) red[wm * BN + wn * (BN / WN) + j * 32 + lane] = sm;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cc = wn * (BN / WN) + j * 32 + frow;
+      float tot = 0.f;
+#pragma unroll
+      for (int k = 0; k < WM; ++k) tot += red[k * BN + cc];
+      const float mean = tot / (float)rows_valid;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          const float d = acc[i][j][v] - mean;
+          if (r < rows_valid) q += d * d;
+        }
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 32) red[WM * BN + wm * BN + cc] = q;
+    }
+    __syncthreads();
+    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
+    for (int cc = tid; cc < BN; cc += NT) {
+      double sd = 0.0, m2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < WM; ++k) {
+        sd += (double)red[k * BN + cc];
+        m2 += (double)red[WM * BN + k * BN + cc];
+      }
+      double* a = acc_slot + (size_t)(n0 + cc) * 3;
+      atomicAdd(a + 0, sd);
+      atomicAdd(a + 1, m2);
+      atomicAdd(a + 2, sd * sd / (double)rows_valid);
+    }
+  }
+  bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        const int cc = wn * (BN / WN) + j * 32 + frow;
+        Ct[r * CT_LD + cc] = f2bf(acc[i][j][v]);
+      }
+  __syncthreads();
+  constexpr int OCPR = BN / 8;
+  for (int idx = tid; idx < BM * OCPR; idx += NT) {
+    const int r = idx / OCPR, cc = idx - r * OCPR;
+    if (r >= rows_valid) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
+    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
+    if (p.add != nullptr) {
+      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+      unsigned* vv = reinterpret_cast<unsigned*>(&v);
+      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
+        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
+        vv[e] = pack2(lo, hi);
+      }
+    }
+    *reinterpret_cast<u32x4*>(p.out + off) = v;
+  }
+}

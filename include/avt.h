@@ -59,6 +59,10 @@ int avt_set_conv_variant(int variant);
  * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
  * — an A/B knob */
 int avt_set_nt64_config(int cfg);
+/* 1 (default; env AVT_HALO): 3x3 stride-1 fwd/dgrad with C % 64 == 0, K % 128 == 0 and W <= 19 (layer3/4)
+ * run on the halo-reuse kernel (each input pixel moved to LDS once per 64-channel chunk instead of once
+ * per tap); 0: tap-gather kernel everywhere; 2: also the 8-wave halo forms for W <= 79 — an A/B knob */
+int avt_set_halo(int on);
 /* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
  * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */

@@ -63,6 +63,13 @@ CONV_CASES = [
     (2, 5, 6, 256, 512, 3, 1, 1),
     (1, 17, 19, 512, 512, 3, 1, 1),
     (2, 15, 13, 64, 128, 1, 2, 0),
+    # halo-reuse kernel shapes (3x3/s1, W up to 79): tiles spanning images, M tails
+    (1, 56, 56, 64, 64, 3, 1, 1),
+    (1, 65, 75, 64, 64, 3, 1, 1),
+    (2, 33, 38, 128, 128, 3, 1, 1),
+    (3, 14, 14, 256, 256, 3, 1, 1),
+    (2, 17, 19, 512, 512, 3, 1, 1),
+    (1, 7, 79, 64, 128, 3, 1, 1),
 ]
 
 
@@ -119,6 +126,7 @@ def test_conv_variants_bitwise_equal(case):
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     dy = _rand_act(N, Pq, Qq, K, 33).to(DEV)
     outs = []
+    call("avt_set_halo", 0)  # the halo kernel sums (chunk, tap) in another order: test_halo_matches_gather
     try:
         for variant in (0, 1):
             call("avt_set_conv_variant", variant)
@@ -147,6 +155,36 @@ def test_conv_variants_bitwise_equal(case):
     finally:
         call("avt_set_nt128_config", -1)
         call("avt_set_nt64_config", 1)
+        call("avt_set_halo", 1)
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[5] == 3 and c[6] == 1])
+def test_halo_matches_gather(case):
+    """Halo-reuse and tap-gather kernels agree to fp32-summation-order noise (bf16 outputs)."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 41).relu().to(DEV)
+    g = torch.Generator().manual_seed(42)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, R * R * C)
+    dy = _rand_act(N, H, W, K, 43).to(DEV)
+    outs = []
+    try:
+        for halo in (0, 1, 2):
+            call("avt_set_halo", halo)
+            y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+            acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
+            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), P(x), N, H, W, C, K, R, R, st, pad, S())
+            torch.cuda.synchronize()
+            outs.append((y.float(), dx.float(), acc.view(-1, K, 3).sum(0)))
+    finally:
+        call("avt_set_halo", 1)
+    (y0, dx0, a0) = outs[0]
+    for y1, dx1, a1 in outs[1:]:  # default halo forms (W <= 19) and the 8-wave A/B forms (W <= 79)
+        assert rel_err(y1, y0) < 1e-2 and rel_err(dx1, dx0) < 1e-2
+        assert (y1 - y0).abs().gt(0).float().mean().item() < 0.1  # mostly bit-equal after bf16 rounding
+        torch.testing.assert_close(a1[:, 0], a0[:, 0], rtol=1e-4, atol=1e-2)
 
 
 @pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
