@@ -61,13 +61,17 @@ SIGNATURES = {
     "avt_hardway_save_floats": (_Z, [_I]),
     "avt_hardway_fwd": (_I, [_P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "avt_hardway_ce": (_I, [_P, _I, _I, _F, _P, _P, _P]),
-    "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P]),
+    "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I,
+                             _P]),
+    "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
+    "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
     "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_pack_desc_bytes": (_Z, []),
     "avt_pack_conv_weights_batched": (_I, [_P, _I, _L, _P]),
     "avt_nchw_to_nhwc_bf16": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "avt_ncthw_to_nhwc_bf16": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "avt_nhwc_bf16_to_nchw": (_I, [_P, _P, _I, _I, _I, _P]),
 }
 

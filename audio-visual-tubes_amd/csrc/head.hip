@@ -37,7 +37,8 @@ __global__ __launch_bounds__(256) void vis_norm_kernel(const bf16_t* __restrict_
 // ---- small fp32 GEMM with strided operands ----
 //   C[m][n] (+)= rowscale[m] * sum_k A(m,k) * kscale[k] * B(k,n)
 //   A(m,k) = a[m*sam + k*sak] (TA = bf16_t or float), B(k,n) = b[k*sbk + n*sbn] (TB)
-//   split-K over gridDim.z with fp32 atomics when gridDim.z > 1 (C pre-zeroed by caller).
+//   split-K over gridDim.z with fp32 atomics when gridDim.z > 1 (C pre-zeroed by caller, or holding
+//   what to add to); accum = 1 adds to C in the single-split case too.
 template <typename T>
 __device__ __forceinline__ float ldf(const T* p, size_t i);
 template <>
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
                                                     long long sak, const TB* __restrict__ b, long long sbk,
                                                     long long sbn, const float* __restrict__ rowscale,
                                                     const float* __restrict__ kscale, float* __restrict__ c,
-                                                    long long ldc, int k_per_split) {
+                                                    long long ldc, int k_per_split, int accum) {
   __shared__ float As[16][64 + 4];
   __shared__ float Bs[16][64 + 4];
   const int tid = threadIdx.x;
@@ -120,6 +121,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
       if (gn >= N) continue;
       if (gridDim.z > 1)
         atomicAdd(c + (size_t)gm * ldc + gn, acc[i][j] * rs);
+      else if (accum)
+        c[(size_t)gm * ldc + gn] += acc[i][j] * rs;
       else
         c[(size_t)gm * ldc + gn] = acc[i][j] * rs;
     }
@@ -257,20 +260,23 @@ __global__ __launch_bounds__(256) void hardway_logits_bwd_kernel(const float* __
 }
 
 // ---- normalize backward for the vision map: gv = inv*(dvh - vh*<vh,dvh>), vh = v*inv ----
+// dm (optional) [rows]: gradient w.r.t. mean_c(vh) (weighted_A path) — adds dm/C to every channel of dvh.
 __global__ __launch_bounds__(256) void vis_norm_bwd_kernel(const bf16_t* __restrict__ v, const float* __restrict__ inv,
-                                                           const float* __restrict__ dvh, bf16_t* __restrict__ gv,
-                                                           int rows, int C) {
+                                                           const float* __restrict__ dvh, const float* __restrict__ dm,
+                                                           bf16_t* __restrict__ gv, int rows, int C) {
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
   if (w >= rows) return;
   const bf16_t* src = v + (size_t)w * C;
   const float* d = dvh + (size_t)w * C;
   const float iv = inv[w];
+  const float dmc = dm ? dm[w] / (float)C : 0.f;
   float dot = 0.f;
   for (int c = lane * 8; c < C; c += 512) {
     const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
     const unsigned* u = reinterpret_cast<const unsigned*>(&q);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dot += bf2f(u[e] & 0xffff) * d[c + 2 * e] + bf2f(u[e] >> 16) * d[c + 2 * e + 1];
+    for (int e = 0; e < 4; ++e)
+      dot += bf2f(u[e] & 0xffff) * (d[c + 2 * e] + dmc) + bf2f(u[e] >> 16) * (d[c + 2 * e + 1] + dmc);
   }
   dot = wave_sum(dot) * iv;  // <vh, dvh>
   for (int c = lane * 8; c < C; c += 512) {
@@ -280,24 +286,139 @@ __global__ __launch_bounds__(256) void vis_norm_bwd_kernel(const bf16_t* __restr
     unsigned* ou = reinterpret_cast<unsigned*>(&o);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float a = iv * (d[c + 2 * e] - bf2f(u[e] & 0xffff) * iv * dot);
-      const float b = iv * (d[c + 2 * e + 1] - bf2f(u[e] >> 16) * iv * dot);
+      const float a = iv * (d[c + 2 * e] + dmc - bf2f(u[e] & 0xffff) * iv * dot);
+      const float b = iv * (d[c + 2 * e + 1] + dmc - bf2f(u[e] >> 16) * iv * dot);
       ou[e] = pack2(a, b);
     }
     *reinterpret_cast<u32x4*>(gv + (size_t)w * C + c) = o;
   }
 }
 
+// ---- weighted_A backward (model.py:148-152): one block per row i ----
+// wA[i,p] = m[i,p] * Pos[i,p] / max(||Pos_i||, 1e-12),  m = mean_c(vh) = vsum*inv/C,
+// Pos = sigmoid((A - eps1)/tau), A[i,p] = A0[i,p,i].  Given g = dwA:
+//   dm[i,p]      = g * Pos * pn                                 (-> every channel of dvh, /C)
+//   dPos         = (u - Pos * pn^2 * <Pos,u>) * pn,  u = g*m    (F.normalize backward, ||Pos|| > eps)
+//                = u * pn                                       (||Pos|| <= eps: clamp_min passes no grad)
+//   dA0[i,p,i]  += dPos * Pos*(1-Pos)/tau                       (A is the diagonal of A0)
+// Runs after hardway_logits_bwd_kernel (read-modify-write of the diagonal it wrote).
+__global__ __launch_bounds__(256) void hardway_wa_bwd_kernel(const float* __restrict__ A0, const float* __restrict__ dwA,
+                                                             const float* __restrict__ vsum,
+                                                             const float* __restrict__ inv, int B, int P, int C,
+                                                             float eps1, float tau, float* __restrict__ dA0,
+                                                             float* __restrict__ dm) {
+  __shared__ float red[16];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const float inv_t = 1.f / tau, invC = 1.f / (float)C;
+  const float* row = A0 + (size_t)i * P * B;
+  const size_t r0 = (size_t)i * P;
+  float pp = 0.f, dot = 0.f;
+  for (int p = tid; p < P; p += blockDim.x) {
+    const float w = sigm((row[(size_t)p * B + i] - eps1) * inv_t);
+    const float m = vsum[r0 + p] * inv[r0 + p] * invC;
+    pp += w * w;
+    dot += w * dwA[r0 + p] * m;
+  }
+  pp = block_sum(pp, red);
+  dot = block_sum(dot, red);
+  const float nrm = sqrtf(pp);
+  const float pn = 1.f / fmaxf(nrm, 1e-12f);
+  const float proj = nrm > 1e-12f ? dot * pn * pn : 0.f;
+  for (int p = tid; p < P; p += blockDim.x) {
+    const size_t d = (size_t)p * B + i;
+    const float w = sigm((row[d] - eps1) * inv_t);
+    const float g = dwA[r0 + p];
+    const float m = vsum[r0 + p] * inv[r0 + p] * invC;
+    const float dpos = (g * m - w * proj) * pn;
+    dA0[(size_t)i * P * B + d] += dpos * w * (1.f - w) * inv_t;
+    dm[r0 + p] = g * w * pn;
+  }
+}
+
+// ---- the 16-frame two-view losses of train_hardway.py:134-142, one block of 1024 threads ----
+//   hardway = lw*CE1, aug = lw*CE2 (CE1/CE2: the hardway_ce outputs), l2 = (100-lw)*MSE(wA1, wA2),
+//   consistency = Prop(wA1) + Prop(wA2),  Prop(x) = mean |x[:,s+1] - x[:,s]| over (clip, s, p)
+//   (losses.py:16-23 with x = weighted.reshape(b, t, h, w)),
+//   combined = (hardway + aug)/2 + l2 + consistency.
+// out[5] = {combined, hardway, aug, l2, consistency}; d1/d2 = d(combined)/d(wA1), d(wA2) (the
+// logits gradients come from hardway_ce with scale lw/2).  wA rows are '(b t)', clip-major.
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(1024) void twoview_loss_kernel(const float* __restrict__ ce1, const float* __restrict__ ce2,
+                                                            const float* __restrict__ w1, const float* __restrict__ w2,
+                                                            int b, int t, int P, float lw, float* __restrict__ out,
+                                                            float* __restrict__ d1, float* __restrict__ d2) {
+  __shared__ float red[16];
+  const long long n = (long long)b * t * P;
+  const float kmse = (100.f - lw) / (float)n;
+  const float kprop = 1.f / ((float)b * (float)(t - 1) * (float)P);
+  float se = 0.f, a1 = 0.f, a2 = 0.f;
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int s = (int)((e / P) % t);
+    const float x1 = w1[e], x2 = w2[e];
+    const float df = x1 - x2;
+    se += df * df;
+    float g1 = 2.f * df * kmse, g2 = -2.f * df * kmse;
+    if (s + 1 < t) {  // diff (s+1) - s
+      const float u1 = w1[e + P] - x1, u2 = w2[e + P] - x2;
+      a1 += fabsf(u1);
+      a2 += fabsf(u2);
+      g1 -= sgnf(u1) * kprop;
+      g2 -= sgnf(u2) * kprop;
+    }
+    if (s > 0) {  // diff s - (s-1)
+      g1 += sgnf(x1 - w1[e - P]) * kprop;
+      g2 += sgnf(x2 - w2[e - P]) * kprop;
+    }
+    d1[e] = g1;
+    d2[e] = g2;
+  }
+  se = block_sum(se, red);
+  a1 = block_sum(a1, red);
+  a2 = block_sum(a2, red);
+  if (threadIdx.x == 0) {
+    const float hard = lw * ce1[0], aug = lw * ce2[0];
+    const float l2 = se * kmse, cons = a1 * kprop + a2 * kprop;
+    out[0] = (hard + aug) * 0.5f + l2 + cons;
+    out[1] = hard;
+    out[2] = aug;
+    out[3] = l2;
+    out[4] = cons;
+  }
+}
+
+// ---- PropagationLoss (losses.py:16-23) on x [b][t][P]: loss and d(loss)/dx, one block ----
+__global__ __launch_bounds__(1024) void propagation_loss_kernel(const float* __restrict__ x, int b, int t, int P,
+                                                                float* __restrict__ loss, float* __restrict__ dx) {
+  __shared__ float red[16];
+  const long long n = (long long)b * t * P;
+  const float k = 1.f / ((float)b * (float)(t - 1) * (float)P);
+  float a = 0.f;
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const int s = (int)((e / P) % t);
+    float g = 0.f;
+    if (s + 1 < t) {
+      const float u = x[e + P] - x[e];
+      a += fabsf(u);
+      g -= sgnf(u) * k;
+    }
+    if (s > 0) g += sgnf(x[e] - x[e - P]) * k;
+    if (dx) dx[e] = g;
+  }
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) *loss = a * k;
+}
+
 template <typename TA, typename TB>
 static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak, const TB* b, long long sbk,
                   long long sbn, const float* rowscale, const float* kscale, float* c, long long ldc, int splits,
-                  hipStream_t st) {
+                  hipStream_t st, int accum = 0) {
   int kps = (K + splits - 1) / splits;
   kps = ((kps + 15) / 16) * 16;
   splits = (K + kps - 1) / kps;
   dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
   hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
-                     kscale, c, ldc, kps);
+                     kscale, c, ldc, kps, accum);
 }
 
 }  // namespace avt
@@ -332,30 +453,54 @@ extern "C" int avt_hardway_ce(const float* logits, int B, int L, float scale, fl
   return check_launch("hardway_ce");
 }
 
-// Backward from dlogits to the trunk outputs.
-//   workspace: dA0 [B][P][B] fp32 + dvh [B][P][C] fp32
+// Backward from dlogits (and optionally d weighted_A) to the trunk outputs.
+//   workspace: dA0 [B][P][B] fp32 + dvh [B][P][C] fp32 (+ dm [B][P] with dwA)
+//   dwA [B][P] (NULL: the logits are the only loss input, the 1-frame step); needs vsum from the
+//   forward and the vision gradient (gv).
 //   outputs: gv [B][P][C] bf16 (grad of the vision layer4 map; dvh = gv = NULL skips it), gan [B][C] fp32
-//   (grad of the unit audio vectors)
+//   (grad of the unit audio vectors; gan_accumulate = 1 adds to gan instead of overwriting it)
 extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
                                const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
-                               int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream) {
+                               int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh,
+                               void* gv, float* gan, int gan_accumulate, void* stream) {
   AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && gan, "hardway_bwd: null pointer");
   AVT_REQUIRE((dvh == nullptr) == (gv == nullptr), "hardway_bwd: dvh and gv must be both set or both null");
+  AVT_REQUIRE(dwA == nullptr || (vsum && dm && gv), "hardway_bwd: dwA needs vsum, dm and the vision gradient");
   hipStream_t st = (hipStream_t)stream;
   const int rows = B * P;
   hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2, tau,
                      trimap, use_neg, dA0);
+  if (dwA != nullptr)
+    hipLaunchKernelGGL(hardway_wa_bwd_kernel, dim3(B), dim3(256), 0, st, A0, dwA, vsum, inv, B, P, C, eps1, tau, dA0, dm);
   // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]   (skipped when the vision map is detached:
   // the tube head, whose video features come from a detached forward hook, model.py:12-15)
   if (gv != nullptr) sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
-  // gan[j][c] = sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
-  (void)hipMemsetAsync(gan, 0, (size_t)B * C * sizeof(float), st);
+  // gan[j][c] (+)= sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
+  if (!gan_accumulate) (void)hipMemsetAsync(gan, 0, (size_t)B * C * sizeof(float), st);
   int splits = rows / 256;
   if (splits < 1) splits = 1;
   if (splits > 64) splits = 64;
-  sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st);
+  sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st, 1);
   if (gv != nullptr)
     hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
-                       (bf16_t*)gv, rows, C);
+                       dwA != nullptr ? dm : nullptr, (bf16_t*)gv, rows, C);
   return check_launch("hardway_bwd");
+}
+
+// The 16-frame two-view loss combination (train_hardway.py:134-142) from the two CE values.
+extern "C" int avt_twoview_loss(const float* ce1, const float* ce2, const float* wA1, const float* wA2, int b, int t,
+                                int P, float loss_weight, float* out, float* dwA1, float* dwA2, void* stream) {
+  AVT_REQUIRE(ce1 && ce2 && wA1 && wA2 && out && dwA1 && dwA2, "twoview_loss: null pointer");
+  AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "twoview_loss: need b >= 1, t >= 2 frames, P >= 1 (b=%d t=%d P=%d)", b, t, P);
+  hipLaunchKernelGGL(twoview_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, ce1, ce2, wA1, wA2, b, t, P,
+                     loss_weight, out, dwA1, dwA2);
+  return check_launch("twoview_loss");
+}
+
+// PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (optional) = d(loss)/dx.
+extern "C" int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream) {
+  AVT_REQUIRE(x && loss, "propagation_loss: null pointer");
+  AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "propagation_loss: need b >= 1, t >= 2, P >= 1 (b=%d t=%d P=%d)", b, t, P);
+  hipLaunchKernelGGL(propagation_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, b, t, P, loss, dx);
+  return check_launch("propagation_loss");
 }

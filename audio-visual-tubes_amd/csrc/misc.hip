@@ -154,15 +154,27 @@ __global__ __launch_bounds__(256) void pack_dgrad_batched_kernel(const PackDesc*
   }
 }
 
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int H, int W,
-                                    int Cp) {
-  const long long total = (long long)N * H * W;
+// x [N][C][T][H][W] fp32 -> y [(N T)][H][W][Cp] bf16 (channels >= C zero): 'b c t h w -> (b t) h w c'
+// (train_hardway.py:130-131 einops fold); T = 1 is plain NCHW -> NHWC.
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int N, int C, int T, int H,
+                                    int W, int Cp) {
+  const long long hw_n = (long long)H * W;
+  const long long total = (long long)N * T * hw_n;
   for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
-    const int n = (int)(t / ((long long)H * W));
-    const long long hw = t % ((long long)H * W);
-    for (int c = 0; c < Cp; ++c) {
-      const float v = c < C ? x[((size_t)n * C + c) * H * W + hw] : 0.f;
-      y[t * Cp + c] = f2bf(v);
+    const long long r = t / hw_n;  // output image (n, tt)
+    const long long hw = t % hw_n;
+    const int n = (int)(r / T), tt = (int)(r % T);
+    const float* src = x + ((size_t)n * C * T + tt) * hw_n + hw;  // + c*T*hw_n
+    if (Cp == 4) {
+      float v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = c < C ? src[(size_t)c * T * hw_n] : 0.f;
+      u32x2 o;
+      o[0] = pack2(v[0], v[1]);
+      o[1] = pack2(v[2], v[3]);
+      *reinterpret_cast<u32x2*>(y + t * 4) = o;
+    } else {
+      for (int c = 0; c < Cp; ++c) y[t * Cp + c] = f2bf(c < C ? src[(size_t)c * T * hw_n] : 0.f);
     }
   }
 }
@@ -275,8 +287,17 @@ extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long
 extern "C" int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream) {
   AVT_REQUIRE(x && y && Cp >= C, "nchw_to_nhwc_bf16: bad arguments");
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)N * H * W)), dim3(256), 0, (hipStream_t)stream, x,
-                     (bf16_t*)y, N, C, H, W, Cp);
+                     (bf16_t*)y, N, C, 1, H, W, Cp);
   return check_launch("nchw_to_nhwc_bf16");
+}
+
+extern "C" int avt_ncthw_to_nhwc_bf16(const float* x, void* y, int N, int C, int T, int H, int W, int Cp,
+                                      void* stream) {
+  AVT_REQUIRE(x && y && Cp >= C && T >= 1, "ncthw_to_nhwc_bf16: bad arguments");
+  AVT_REQUIRE(Cp != 4 || ((uintptr_t)y & 7) == 0, "ncthw_to_nhwc_bf16: y must be 8-byte aligned");
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for((long long)N * T * H * W)), dim3(256), 0, (hipStream_t)stream,
+                     x, (bf16_t*)y, N, C, T, H, W, Cp);
+  return check_launch("ncthw_to_nhwc_bf16");
 }
 
 extern "C" int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream) {

@@ -285,7 +285,7 @@ class AVEngine:
         tape = None
         if training:
             tape = {"img": tape_i, "aud": tape_a, "v": v, "a": a, "an": an, "amax": amax, "anorm": anorm,
-                    "inv": inv, "A0": A0, "save": save, "B": B, "P": Pn, "C": C}
+                    "inv": inv, "vsum": vsum, "A0": A0, "save": save, "B": B, "P": Pn, "C": C}
         if with_ce:
             loss = torch.empty((), **f32)
             dlogits = torch.empty(B, L, **f32) if training else None
@@ -318,20 +318,38 @@ class AVEngine:
     def backward_order(self):
         return [self.img, self.aud]
 
-    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor, on_boundary=None):
-        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).  on_boundary(tag)
-        is called as each grad_buckets() bucket becomes final (for an overlapped all-reduce)."""
+    def head_backward(self, tape, dlogits: Optional[torch.Tensor], dwA: Optional[torch.Tensor] = None,
+                      gan: Optional[torch.Tensor] = None):
+        """Hard-way head backward: (d logits, d weighted_A) -> (gv [B,h,w,C] bf16, gan [B,C] fp32).
+        A given ``gan`` is accumulated into (two views sharing one audio batch)."""
         B, Pn, C = tape["B"], tape["P"], tape["C"]
-        dev = dlogits.device
+        dev = tape["v"].device
         f32 = dict(device=dev, dtype=torch.float32)
+        L = B + (2 if self.neg else 1)
+        dlogits = torch.zeros(B, L, **f32) if dlogits is None else dlogits.contiguous().float()
         dA0 = torch.empty(B, Pn, B, **f32)
         dvh = torch.empty(B, Pn, C, **f32)
         gv = torch.empty_like(tape["v"])
-        gan = torch.empty(B, C, **f32)
-        dlogits = dlogits.contiguous().float()
+        accumulate = gan is not None
+        if gan is None:
+            gan = torch.empty(B, C, **f32)
+        dm = None
+        if dwA is not None:
+            dwA = dwA.contiguous().float()
+            dm = torch.empty(B, Pn, **f32)
         call("avt_hardway_bwd", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
-             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map), int(self.neg), P(dA0),
-             P(dvh), P(gv), P(gan), stream_ptr())
+             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map), int(self.neg), P(dwA),
+             P(tape["vsum"] if dwA is not None else None), P(dm), P(dA0), P(dvh), P(gv), P(gan), int(accumulate),
+             stream_ptr())
+        return gv, gan
+
+    def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
+                 dwA: Optional[torch.Tensor] = None):
+        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).  on_boundary(tag)
+        is called as each grad_buckets() bucket becomes final (for an overlapped all-reduce).
+        dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141)."""
+        B, C = tape["B"], tape["C"]
+        gv, gan = self.head_backward(tape, dlogits, dwA)
         a = tape["a"]
         ga = torch.empty_like(a)
         call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,

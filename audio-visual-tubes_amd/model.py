@@ -4,7 +4,7 @@ Same constructor (``AVENet(args, pretrained)``; args needs epsilon, epsilon2, tr
 module tree and state_dict keys (``imgnet.*`` / ``audnet.*`` incl. the unused ``conv1_flow``,
 other-modality stem and ``fc``), same init rule and RNG consumption order (so
 ``torch.manual_seed(s)`` gives the reference's weights), same forward signature and outputs
-``(A, logits, weighted_A, Pos, Neg)``; gradients flow from ``logits`` through autograd into the
+``(A, logits, weighted_A, Pos, Neg)``; gradients flow from ``logits`` and ``weighted_A`` through autograd into the
 Parameters.  Compute runs in libavt (HIP, gfx950); there is no CPU path.
 """
 from __future__ import annotations
@@ -98,20 +98,23 @@ class _AVENetFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gA, glogits, gwA, gPos, gNeg):
-        for name, g in (("A", gA), ("weighted_A", gwA), ("Pos", gPos), ("Neg", gNeg)):
+        # the reference's train scripts back-propagate logits (CE, train_hardway_1frame.py:130-131) and
+        # weighted_A (MSE + PropagationLoss, train_hardway.py:138-141); A/Pos/Neg only feed eval/logging
+        for name, g in (("A", gA), ("Pos", gPos), ("Neg", gNeg)):
             if g is not None and bool(torch.any(g != 0)):
                 raise NotImplementedError(
-                    f"avt: gradients through `{name}` are not implemented yet (the 1-frame hard-way "
-                    "step only back-propagates the logits; see DESIGN.md §next)")
+                    f"avt: gradients through `{name}` are not implemented (no reference train script "
+                    "back-propagates it; see DESIGN.md)")
         engine: AVEngine = ctx.engine
         if ctx.tape is None:
-            raise RuntimeError("avt: backward through an eval-mode forward")
+            raise RuntimeError("avt: backward through an eval-mode forward (or a second backward)")
         nparams = ctx.n_params
-        if glogits is None:
+        if glogits is None and gwA is None:
             return (None, None, None, None) + (None,) * nparams
         flat = engine.flat
-        gflat = torch.zeros(flat.n_train, device=glogits.device, dtype=torch.float32)
-        engine.backward(ctx.tape, glogits, gflat)
+        dev = (glogits if glogits is not None else gwA).device
+        gflat = torch.zeros(flat.n_train, device=dev, dtype=torch.float32)
+        engine.backward(ctx.tape, glogits, gflat, dwA=gwA)
         ctx.tape = None
         views = flat.param_grad_views(gflat)
         grads = tuple(views.get(n) for n in flat.pnames[:nparams])

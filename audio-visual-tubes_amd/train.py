@@ -49,9 +49,9 @@ def sync_buffers(bflat: torch.Tensor, pg: Optional[dist.ProcessGroup] = None):
 
 class HardWayTrainStep:
     def __init__(self, model, lr: float = 1e-6, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 process_group: Optional[dist.ProcessGroup] = None):
+                 process_group: Optional[dist.ProcessGroup] = None, engine=None):
         self.model = model
-        self.engine: AVEngine = model.engine()
+        self.engine: AVEngine = engine if engine is not None else model.engine()
         self.flat = model._flat
         self.opt = FlatAdam(self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         self.grad = torch.zeros(self.flat.n_train, device=self.flat.flat.device, dtype=torch.float32)
@@ -66,7 +66,8 @@ class HardWayTrainStep:
         self._seg_graphs = None
         self.buckets = dict(self.engine.grad_buckets())  # boundary tag -> flat gradient region
 
-    def _fwd_bwd(self, image: torch.Tensor, audio: torch.Tensor, on_boundary=None) -> torch.Tensor:
+    def _fwd_bwd(self, *inputs, on_boundary=None) -> torch.Tensor:
+        image, audio = inputs
         out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
         self.grad.zero_()
         self.engine.backward(tape, out["dlogits"], self.grad, on_boundary)
@@ -76,23 +77,23 @@ class HardWayTrainStep:
         lo, hi = self.buckets[tag]
         works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
-    def step(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
-        """Returns the local mean CE loss (device scalar, no host sync)."""
+    def step(self, *inputs: torch.Tensor) -> torch.Tensor:
+        """step(image, audio).  Returns the local mean CE loss (device scalar, no host sync)."""
         if self._graph is not None or self._seg_graphs is not None:
-            return self._replay(image, audio)
+            return self._replay(*inputs)
         if self.world == 1:
-            loss = self._fwd_bwd(image, audio)
+            loss = self._fwd_bwd(*inputs)
             self.opt.step(self.grad, grad_scale=1.0)
             return loss
         sync_buffers(self.flat.bflat, self.pg)
         works: list = []
-        loss = self._fwd_bwd(image, audio, lambda tag: self._allreduce_bucket(tag, works))
+        loss = self._fwd_bwd(*inputs, on_boundary=lambda tag: self._allreduce_bucket(tag, works))
         for w in works:  # the current stream waits for RCCL's (no host sync)
             w.wait()
         self.opt.step(self.grad, grad_scale=1.0 / self.world)
         return loss
 
-    def capture(self, image: torch.Tensor, audio: torch.Tensor) -> None:
+    def capture(self, *inputs: torch.Tensor) -> None:
         """Record one step into HIP graph(s) (torch.cuda.CUDAGraph is hipGraph on ROCm) so that
         later steps are replays: no per-kernel host launch cost and no launch gaps between the
         ~700 kernels of a step.  World 1: one graph (fwd + CE + bwd + Adam).  World > 1: the RCCL
@@ -101,11 +102,11 @@ class HardWayTrainStep:
         Call after at least one eager step (the engine allocates its buffers lazily).  Capture
         records launches without running them, so it has no effect on the training state."""
         torch.cuda.synchronize()
-        self._static_in = (image, audio)
+        self._static_in = inputs
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                loss = self._fwd_bwd(image, audio)
+                loss = self._fwd_bwd(*inputs)
                 self.opt.step(self.grad, grad_scale=1.0)
             self._static_loss = loss
             self._graph = g
@@ -129,7 +130,7 @@ class HardWayTrainStep:
                     g2.capture_begin(pool=pool)
                     graphs.append(g2)
 
-            loss = self._fwd_bwd(image, audio, boundary)
+            loss = self._fwd_bwd(*inputs, on_boundary=boundary)
             if not tags or tags[-1] != last_tag:
                 raise RuntimeError("avt: backward did not reach its last gradient bucket")
             g_opt = torch.cuda.CUDAGraph()
@@ -141,12 +142,10 @@ class HardWayTrainStep:
         self._static_loss = loss
         self._seg_graphs, self._seg_tags, self._graph_opt = graphs, tags, g_opt
 
-    def _replay(self, image: torch.Tensor, audio: torch.Tensor) -> torch.Tensor:
-        si, sa = self._static_in
-        if image is not si:
-            si.copy_(image)
-        if audio is not sa:
-            sa.copy_(audio)
+    def _replay(self, *inputs: torch.Tensor) -> torch.Tensor:
+        for s, x in zip(self._static_in, inputs):
+            if x is not s:
+                s.copy_(x)
         if self._seg_graphs is not None:
             sync_buffers(self.flat.bflat, self.pg)
             works: list = []
@@ -159,3 +158,30 @@ class HardWayTrainStep:
         else:
             self._graph.replay()
         return self._static_loss
+
+
+class TwoViewTrainStep(HardWayTrainStep):
+    """One train_hardway.py iteration (126-145): ``step(frames, augmented, spec)`` with frames /
+    augmented [b,3,t,H,W] and one spectrogram per clip [b,1,F,T]; returns the device tensor
+    losses[5] = (combined, hardway, aug, l2, consistency) — the five terms the reference logs.
+    Defaults are train_hardway.py's: Adam lr 4e-6, weight_decay 1e-4, loss_weight 0.1.  Data
+    parallel as HardWayTrainStep (each rank: its own clips, local negatives)."""
+
+    def __init__(self, model, lr: float = 4e-6, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 loss_weight: float = 0.1, dedup_audio: bool = True,
+                 process_group: Optional[dist.ProcessGroup] = None):
+        from .twoview import TwoViewEngine
+
+        # its own engine (packed weights, BN arena) over the model's flat storage: model(image, audio)
+        # keeps working alongside
+        e = TwoViewEngine(model._flat, model.epsilon, model.epsilon2, model.tau, model.trimap, model.Neg,
+                          loss_weight=loss_weight, dedup_audio=dedup_audio)
+        super().__init__(model, lr=lr, weight_decay=weight_decay, betas=betas, eps=eps, process_group=process_group,
+                         engine=e)
+
+    def _fwd_bwd(self, *inputs, on_boundary=None) -> torch.Tensor:
+        frames, augmented, spec = inputs
+        out, tape = self.engine.forward(frames, augmented, spec, training=True, with_ce=True)
+        self.grad.zero_()
+        self.engine.backward(tape, (out["dlogits"], out["dwA"]), self.grad, on_boundary)
+        return out["losses"]

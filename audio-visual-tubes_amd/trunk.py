@@ -127,7 +127,7 @@ def _bn_finalize(c_out, acc, rows, bn: BNSpec, store: Store, training: bool, mom
     stats = torch.empty(4, C, device=c_out.device, dtype=torch.float32)  # scale, shift, mean, invstd
     gamma = store.param(bn.prefix + ".weight")
     beta = store.param(bn.prefix + ".bias")
-    if training and rep > 1:
+    if training and (rep > 1 or momentum != 0.1):
         call("avt_bn_finalize_rep", P(acc), rows, rep, C, P(gamma), P(beta),
              P(store.buffer(bn.prefix + ".running_mean")), P(store.buffer(bn.prefix + ".running_var")),
              ctypes.c_float(momentum), ctypes.c_float(eps), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]),
@@ -154,6 +154,7 @@ class Trunk:
     def __init__(self, prefix: str, modal: str):
         self.prefix, self.modal = prefix, modal
         self.bn_rep = 1  # >1: each input sample stands for bn_rep identical ones (tube audio de-dup)
+        self.bn_momentum = 0.1  # 0.19: two reference forwards over the same batch in one (two-view audio)
         if modal == "audio":
             self.stem = ConvSpec(prefix + "conv1_a.weight", 1, 64, 7, 2, 3, 1)
         else:
@@ -203,7 +204,7 @@ class Trunk:
              spec.stride, spec.pad, spec.kg, stream_ptr())
         ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + wf.numel() + y.numel()))
-        stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, rep=self.bn_rep)
+        stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, momentum=self.bn_momentum, rep=self.bn_rep)
         return y, stats, Pq, Qq
 
     def forward(self, x: torch.Tensor, store: Store, training: bool):

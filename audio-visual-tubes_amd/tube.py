@@ -274,8 +274,8 @@ class TubeEngine(AVEngine):
         gan = torch.empty(B, C, **f32)
         dlogits = dlogits.contiguous().float()
         call("avt_hardway_bwd", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
-             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, P(dA0), None, None, P(gan),
-             stream_ptr())
+             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, None, None, None, P(dA0), None, None,
+             P(gan), 0, stream_ptr())
         if rep > 1:
             gan_a = torch.empty(Ba, C, **f32)
             call("avt_sum_rep_rows_f32", P(gan), P(gan_a), Ba, rep, C, stream_ptr())

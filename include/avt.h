@@ -28,6 +28,10 @@
  *   avt_pack_conv3d_weight       32-channel Conv2d over the frames (temporal taps folded into channels)
  *   avt_bn_finalize_rep          BatchNorm2d over the t-fold repeated spectrogram batch (train_3D.py:128-130)
  *                                computed once per distinct clip
+ *   avt_twoview_loss             the 16-frame two-view loss of train_hardway.py:134-142: lw*CE x2, (100-lw)*
+ *                                nn.MSELoss(weighted, weighted2), PropagationLoss x2 (losses.py:16-23)
+ *   avt_propagation_loss         PropagationLoss.forward (losses.py:22-23) + its gradient
+ *   avt_ncthw_to_nhwc_bf16       einops 'b c t h w -> (b t) c h w' of the frames (train_hardway.py:130-131)
  */
 #ifndef AVT_H_
 #define AVT_H_
@@ -153,10 +157,22 @@ int avt_hardway_fwd(const void* v, const float* an, int B, int P, int C, float e
                     int use_neg, float* inv, float* vsum, float* A0, float* save, float* logits, float* Aout,
                     float* Pos, float* Neg, float* wA, void* stream);
 int avt_hardway_ce(const float* logits, int B, int L, float scale, float* loss, float* dlogits, void* stream);
-/* dvh = gv = NULL: no vision gradient (detached video features of the tube head) */
+/* dvh = gv = NULL: no vision gradient (detached video features of the tube head).
+ * dwA [B][P] (or NULL): upstream gradient of weighted_A (model.py:148-152; train_hardway.py:138-141
+ * back-propagates it), needs the forward's vsum and a dm [B][P] workspace.
+ * gan_accumulate = 1: gan += (two views sharing one audio batch) instead of gan = */
 int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
                     const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
-                    int use_neg, float* dA0, float* dvh, void* gv, float* gan, void* stream);
+                    int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh, void* gv,
+                    float* gan, int gan_accumulate, void* stream);
+/* train_hardway.py:134-142 loss combination of the 16-frame two-view step: given the two CE values
+ * (avt_hardway_ce outputs; their dlogits use scale loss_weight/2) and weighted_A of both views
+ * ([b*t][P], '(b t)' clip-major), out[5] = {combined, hardway, aug, l2, consistency} and
+ * dwA1/dwA2 = d(combined)/d(weighted_A).  losses.py:16-23 PropagationLoss + nn.MSELoss. */
+int avt_twoview_loss(const float* ce1, const float* ce2, const float* wA1, const float* wA2, int b, int t, int P,
+                     float loss_weight, float* out, float* dwA1, float* dwA2, void* stream);
+/* PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (or NULL) = d(loss)/dx */
+int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
 
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
@@ -173,6 +189,9 @@ int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int
 size_t avt_pack_desc_bytes(void);
 int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream);
 int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream);
+/* x [N][C][T][H][W] fp32 -> y [(N T)][H][W][Cp] bf16: the 'b c t h w -> (b t) c h w' fold of
+ * train_hardway.py:130-131 fused with the NHWC/bf16 conversion */
+int avt_ncthw_to_nhwc_bf16(const float* x, void* y, int N, int C, int T, int H, int W, int Cp, void* stream);
 int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream);
 
 #ifdef __cplusplus

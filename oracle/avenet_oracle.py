@@ -22,6 +22,9 @@ What it restates (reference file:line):
   * Adam(lr, betas (0.9,0.999), eps 1e-8, coupled L2 weight_decay) —
     train_hardway_1frame.py:116,134 (torch.optim.Adam semantics).
   * nn.DataParallel semantics: per-replica local negatives — model.py:114-115.
+  * The 16-frame two-view step: frame/spectrogram folding, two forwards, lw*CE x2,
+    (100-lw)*MSE(weighted_A, weighted_A_aug), PropagationLoss x2 — train_hardway.py:126-144,
+    losses.py:16-23 (restated from text: losses.py is not importable).
 """
 from __future__ import annotations
 
@@ -304,3 +307,69 @@ def train_step(sd, image, audio, opt: AdamRef = None, args: Args = None):
         with torch.no_grad():
             opt.step({n: sd[n] for n in names}, grads)
     return loss.detach(), logits.detach(), grads
+
+
+# --------------------------------------------------------------------------------------
+# 16-frame two-view step (train_hardway.py:126-144)
+# --------------------------------------------------------------------------------------
+
+def propagation_loss(heatmap: torch.Tensor) -> torch.Tensor:
+    """PropagationLoss.forward (losses.py:22-23) on heatmap [b, t, h, w].  losses.py is not
+    importable here (`from turtle import pos`, pytorch_metric_learning, torchvision: SURVEY §8c),
+    so this one-liner is restated from its text."""
+    return torch.abs(torch.diff(heatmap, dim=1)).mean(dim=(2, 3)).mean(dim=1).mean(dim=0)
+
+
+def twoview_losses(out1, out2, b: int, t: int, loss_weight: float = 0.1):
+    """train_hardway.py:134-142 given the two AVENet outputs (A, logits, weighted_A, Pos, Neg).
+    weighted.reshape(batch_size, frame_density, 14, 14) is written for the layer4 map's own (h, w).
+    Returns (combined, hardway, aug, l2, consistency)."""
+    _, logits1, w1, _, _ = out1
+    _, logits2, w2, _, _ = out2
+    hardway = hardway_ce(logits1) * loss_weight
+    aug = hardway_ce(logits2) * loss_weight
+    l2 = F.mse_loss(w1, w2) * (100 - loss_weight)
+    h, w = w1.shape[-2:]
+    consistency = propagation_loss(w1.reshape(b, t, h, w)) + propagation_loss(w2.reshape(b, t, h, w))
+    combined = (hardway + aug) / 2 + l2 + consistency
+    return combined, hardway, aug, l2, consistency
+
+
+def fold_frames(frames: torch.Tensor) -> torch.Tensor:
+    """einops 'b c t h w -> (b t) c h w' (train_hardway.py:130-131)."""
+    b, c, t, h, w = frames.shape
+    return frames.permute(0, 2, 1, 3, 4).reshape(b * t, c, h, w)
+
+
+def fold_spec(spec: torch.Tensor, t: int) -> torch.Tensor:
+    """spec.unsqueeze(2).repeat(1, 1, t, 1, 1) then 'b c t h w -> (b t) c h w' (train_hardway.py:128-129)."""
+    return fold_frames(spec.unsqueeze(2).repeat(1, 1, t, 1, 1))
+
+
+def twoview_step(sd, frames, augmented, spec, opt: AdamRef = None, args: Args = None, loss_weight: float = 0.1):
+    """One train_hardway.py step (126-144): two AVENet forwards (frames, augmented) on the 16x
+    repeated spectrogram, the combined loss, backward, Adam.  Mutates ``sd`` (BN buffers are updated
+    by both forwards; Adam if ``opt``).  frames/augmented [b,3,t,H,W], spec [b,1,F,T].
+    Returns (losses (combined, hardway, aug, l2, consistency), out1, out2, grads)."""
+    b, t = frames.shape[0], frames.shape[2]
+    names = trainable_names(sd)
+    leaves = {n: sd[n].detach().clone().requires_grad_(True) for n in names}
+    work = OrderedDict(sd)
+    work.update(leaves)
+    aud = fold_spec(spec, t)
+    out1 = avenet_forward(work, fold_frames(frames), aud, args, training=True)
+    out2 = avenet_forward(work, fold_frames(augmented), aud, args, training=True)
+    losses = twoview_losses(out1, out2, b, t, loss_weight)
+    gl = torch.autograd.grad(losses[0], [leaves[n] for n in names])
+    grads = {n: g for n, g in zip(names, gl)}
+    if opt is not None:
+        with torch.no_grad():
+            opt.step({n: sd[n] for n in names}, grads)
+    return (tuple(x.detach() for x in losses), tuple(o.detach() for o in out1), tuple(o.detach() for o in out2),
+            grads)
+
+
+def make_frames(b: int, t: int, size: int = 224, seed: int = 3) -> torch.Tensor:
+    """Seeded synthetic clip frames [b,3,t,H,W] (ImageNet-normalised range, like make_image)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return torch.from_numpy(rng.standard_normal((b, 3, t, size, size), dtype=np.float32))

@@ -35,6 +35,22 @@ def S():
 
 
 DEV = "cuda"
+_KEEP = []  # device copies passed straight into a call(): referenced until the test ends
+
+
+@pytest.fixture(autouse=True)
+def _release_kept():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def D(t):
+    """t on the GPU, kept alive: a temporary freed while its kernel is still queued (or whose block
+    the caching allocator hands to the next argument) would alias another operand."""
+    d = t.to(DEV)
+    _KEEP.append(d)
+    return d
 
 
 def rel_err(a, b):
@@ -224,7 +240,7 @@ def test_conv_dgrad(case):
     w = (torch.randn(K, R, R, C, generator=g) * 0.05).float()
     _, wt = pack(w.to(DEV), C, R * R * C)
     dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
-    call("avt_conv2d_dgrad", P(dy.to(DEV)), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+    call("avt_conv2d_dgrad", P(D(dy)), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
     ref = torch.nn.grad.conv2d_input((N, C, H, W), w.to(torch.bfloat16).double().permute(0, 3, 1, 2),
                                      dy.double().permute(0, 3, 1, 2), stride=st, padding=pad).permute(0, 2, 3, 1)
     torch.cuda.synchronize()
@@ -232,7 +248,7 @@ def test_conv_dgrad(case):
     # accumulate path: dx2 = dgrad + add
     add = _rand_act(N, H, W, C, 7)
     dx2 = torch.empty_like(dx)
-    call("avt_conv2d_dgrad", P(dy.to(DEV)), P(wt), P(dx2), P(add.to(DEV)), N, H, W, C, K, R, R, st, pad, S())
+    call("avt_conv2d_dgrad", P(D(dy)), P(wt), P(dx2), P(D(add)), N, H, W, C, K, R, R, st, pad, S())
     torch.cuda.synchronize()
     assert rel_err(dx2, ref + add.double()) < 8e-3
 
@@ -306,10 +322,10 @@ def test_bn_forward_train(shape):
     stats = torch.empty(4, C, device=DEV)
     rmd, rvd = rm.to(DEV), rv.to(DEV)
     rows = N * H * W
-    call("avt_bn_finalize", P(acc), rows, C, P(gamma.to(DEV)), P(beta.to(DEV)), P(rmd), P(rvd),
+    call("avt_bn_finalize", P(acc), rows, C, P(D(gamma)), P(D(beta)), P(rmd), P(rvd),
          ctypes.c_float(0.1), ctypes.c_float(1e-5), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
     out = torch.empty_like(c, device=DEV)
-    call("avt_bn_apply", P(c.to(DEV)), P(stats[0]), P(stats[1]), P(res.to(DEV)), None, None, P(out), rows, C, 1, S())
+    call("avt_bn_apply", P(D(c)), P(stats[0]), P(stats[1]), P(D(res)), None, None, P(out), rows, C, 1, S())
     torch.cuda.synchronize()
     cn = c.double().permute(0, 3, 1, 2)
     rm64, rv64 = rm.double(), rv.double()
@@ -345,8 +361,8 @@ def test_bn_backward(shape, masked):
     dbeta = torch.zeros(C, device=DEV)
     gc = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
     gmask = torch.empty_like(gc)
-    call("avt_bn_bwd", P(gy.to(DEV)), P(yd if masked else None), P(c.to(DEV)), P(mean.float().to(DEV)),
-         P(inv.float().to(DEV)), P(gamma.to(DEV)), P(dgamma), P(dbeta), P(gc), P(gmask), P(ws), rows, C, S())
+    call("avt_bn_bwd", P(D(gy)), P(yd if masked else None), P(D(c)), P(D(mean.float())),
+         P(D(inv.float())), P(D(gamma)), P(dgamma), P(dbeta), P(gc), P(gmask), P(ws), rows, C, S())
     torch.cuda.synchronize()
     assert rel_err(gc, cn.grad.permute(0, 2, 3, 1)) < 2e-2
     assert rel_err(dgamma, gm.grad) < 1e-2
@@ -439,8 +455,8 @@ def test_stem_fused(shape):
     ws = torch.zeros(int(query("avt_bn_bwd_workspace", N * H * W, C)), device=DEV, dtype=torch.uint8)
     dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
     gc = torch.empty_like(cd)
-    call("avt_stem_maxpool_bn_relu_bwd", P(gy.to(DEV)), P(idx), P(carg), P(cd), P(st[0]), P(st[1]), P(st[2]),
-         P(st[3]), P(gamma.to(DEV)), P(dgamma), P(dbeta), P(gc), P(ws), N, H, W, C, S())
+    call("avt_stem_maxpool_bn_relu_bwd", P(D(gy)), P(idx), P(carg), P(cd), P(st[0]), P(st[1]), P(st[2]),
+         P(st[3]), P(D(gamma)), P(dgamma), P(dbeta), P(gc), P(ws), N, H, W, C, S())
     torch.cuda.synchronize()
     assert not ws[: 16 * C * 2 * 8].any()
     cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
@@ -469,7 +485,7 @@ def test_maxpool(shape):
     call("avt_maxpool3s2_fwd", P(xd), P(y), P(idx), N, H, W, C, S())
     gy = _rand_act(N, P2, Q2, C, 19)
     gx = torch.empty_like(xd)
-    call("avt_maxpool3s2_bwd", P(gy.to(DEV)), P(idx), P(gx), N, H, W, C, S())
+    call("avt_maxpool3s2_bwd", P(D(gy)), P(idx), P(gx), N, H, W, C, S())
     xn = x.double().permute(0, 3, 1, 2).requires_grad_(True)
     yr = F.max_pool2d(xn, 3, 2, 1)
     yr.backward(gy.double().permute(0, 3, 1, 2))
@@ -493,7 +509,7 @@ def test_audio_pool_norm(B, HW, C):
     g = torch.Generator().manual_seed(21)
     gan = torch.randn(B, C, generator=g)
     ga = torch.empty_like(ad)
-    call("avt_audio_pool_norm_bwd", P(gan.to(DEV)), P(an), P(amax), P(anorm), P(ga), B, HW, C, S())
+    call("avt_audio_pool_norm_bwd", P(D(gan)), P(an), P(amax), P(anorm), P(ga), B, HW, C, S())
     at = a.double().permute(0, 2, 1).reshape(B, C, HW, 1).requires_grad_(True)
     r = F.normalize(F.adaptive_max_pool2d(at, 1).flatten(1), dim=1)
     r.backward(gan.double())
@@ -536,7 +552,7 @@ def test_hardway_head(B, h, w, trimap, neg):
     gv = torch.empty_like(vd)
     gan = torch.empty(B, C, **dev)
     call("avt_hardway_bwd", P(vd), P(and_), P(inv), P(A0), P(save), P(dl), B, Pn, C, 0.65, 0.4, 0.03, int(trimap),
-         int(neg), P(dA0), P(dvh), P(gv), P(gan), S())
+         int(neg), None, None, None, P(dA0), P(dvh), P(gv), P(gan), 0, S())
     torch.cuda.synchronize()
     # fp64 oracle on the same (bf16) features
     vt = v.double().permute(0, 3, 1, 2).requires_grad_(True)
@@ -600,6 +616,6 @@ def test_adam_matches_torch():
     for t in range(1, 4):
         gr = torch.randn(n, generator=g)
         opt.step(pr, {"p": gr.double()})
-        call("avt_adam_step", P(pd), P(gr.to(DEV)), P(m), P(v), n, 1.0, 1e-3, 0.9, 0.999, 1e-8, 1e-4, t, S())
+        call("avt_adam_step", P(pd), P(D(gr)), P(m), P(v), n, 1.0, 1e-3, 0.9, 0.999, 1e-8, 1e-4, t, S())
     torch.cuda.synchronize()
     assert rel_err(pd - p0.to(DEV), pr["p"] - p0.double()) < 1e-4
