@@ -1,6 +1,6 @@
 """Train-step clips/s of the audio-visual hard-way step (BASELINE.json metric) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload 1frame|tube]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--workload 1frame|tube|twoview]
                     [--no-cpu-baseline]
     (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
@@ -13,6 +13,12 @@ local negatives and one RCCL all-reduce of the 89.4 MB fp32 gradient per step.
 spectrogram each; R3D-18 forward (detached, as the reference's hook) + audio ResNet-18 fwd/bwd over
 the 16-fold repeated spectrogram (run once per clip unless --tube-folded: exact, tube.py) + the
 hard-way head over the (b t) = 128 rows + CE + Adam.
+
+--workload twoview (train_hardway.py, the 16-frame two-view step): per GPU b=8 clips of 16x224x224
+frames in two views (frames, augmented) + one 257x300 spectrogram each; two AVENet forwards over the
+(b t) = 128 frames of each view, 0.1*CE x2 + 99.9*MSE(weighted_A) + PropagationLoss x2, backward,
+Adam (lr 4e-6).  The audio trunk runs once per clip for both views unless --twoview-folded (exact:
+twoview.py); a clip counts once however many frames/views it has.
 
 Inputs are synthetic and already resident in HBM when the timed region starts; weights are
 random-init (no checkpoints).  Prints ONE JSON line on rank 0.  `roofline` is for the dominant
@@ -54,7 +60,8 @@ def synthetic_inputs(B, device, seed, frames=0):
 
 
 def traffic_file(workload, B):
-    return os.path.join(REPO, "profiles", f"conv_traffic_{'b' if workload == '1frame' else 'tube_b'}{B}.json")
+    tag = {"1frame": "b", "tube": "tube_b", "twoview": "twoview_b"}[workload]
+    return os.path.join(REPO, "profiles", f"conv_traffic_{tag}{B}.json")
 
 
 def conv_traffic(path, launches_per_step, B):
@@ -100,6 +107,15 @@ def cpu_baseline(workload: str, budget_s: float = 20.0):
 
     cores = _cores()
     torch.set_num_threads(cores)
+    if workload == "twoview":
+        t = 16
+        sd = orc.make_state(0)
+        fr, au, sp = orc.make_frames(1, t, 224, seed=3), orc.make_frames(1, t, 224, seed=4), orc.make_spectrogram(1)
+        opt = orc.AdamRef(lr=4e-6)
+        med, n = _time_loop(lambda: orc.twoview_step(sd, fr, au, sp, opt), budget_s, max_n=10)
+        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port",
+                "sample": f"oracle fp32 train_hardway step (two views x 16 frames of 224^2, 16x-repeated 257x300 "
+                          f"spectrogram, both AVENet forwards + 3 losses + backward + Adam), b=1 clip, median of {n}"}
     if workload == "tube":
         import tube_oracle as tor
 
@@ -124,9 +140,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["1frame", "tube"], default="1frame")
-    ap.add_argument("--batch", type=int, default=0, help="clips per GPU (default 128; tube: 8)")
-    ap.add_argument("--frames", type=int, default=16, help="tube: frames per clip")
+    ap.add_argument("--workload", choices=["1frame", "tube", "twoview"], default="1frame")
+    ap.add_argument("--batch", type=int, default=0, help="clips per GPU (default 128; tube, twoview: 8)")
+    ap.add_argument("--frames", type=int, default=16, help="tube, twoview: frames per clip")
+    ap.add_argument("--twoview-folded", action="store_true", help="twoview: run the audio trunk over the folded "
+                    "16x-repeated spectrogram batch once per view (the reference's arithmetic)")
     ap.add_argument("--tube-folded", action="store_true", help="tube: run the audio trunk over the folded "
                     "16x-repeated spectrogram batch (the reference's arithmetic) instead of once per clip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -147,57 +165,69 @@ def main():
 
     import avtubes  # noqa: F401
     from avt_amd.model import AVENet, FullModel
-    from avt_amd.train import HardWayTrainStep
+    from avt_amd.train import HardWayTrainStep, TwoViewTrainStep
     from avt_amd.trunk import ConvProfiler
 
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import avenet_oracle as orc
 
     tube = args.workload == "tube"
-    B = args.batch or (8 if tube else 128)
+    twoview = args.workload == "twoview"
+    B = args.batch or (8 if (tube or twoview) else 128)
     torch.manual_seed(0)
-    if tube:
+    if twoview:
+        model = AVENet(orc.Args(), False).to(dev).train()
+        frames, spec = synthetic_inputs(B, dev, seed=1000 + rank, frames=args.frames)
+        augmented, _ = synthetic_inputs(B, dev, seed=2000 + rank, frames=args.frames)
+        inputs = (frames, augmented, spec)
+        workload = (f"train_hardway step: b={B} clips x {args.frames} frames of 224x224 in two views + 257x300 "
+                    f"spectrogram ({'folded (b t) batch per view' if args.twoview_folded else 'audio once per clip'}),"
+                    f" two AVENet forwards over (b t)={B * args.frames} rows, CE x2 + MSE + PropagationLoss, bwd, Adam")
+    elif tube:
         model = FullModel(orc.Args()).to(dev).train()
         video, spec = synthetic_inputs(B, dev, seed=1000 + rank, frames=args.frames)
         if args.tube_folded:  # train_3D.py:128-130
             spec = spec.unsqueeze(2).repeat(1, 1, args.frames, 1, 1).transpose(1, 2).reshape(
                 B * args.frames, 1, 257, 300).contiguous()
-        x1, x2 = spec, video
+        inputs = (spec, video)
         workload = (f"train_3D step: b={B} clips of {args.frames}x224x224 frames + 257x300 spectrogram, R3D-18 fwd "
                     f"+ audio ResNet-18 fwd/bwd ({'folded (b t) batch' if args.tube_folded else 'once per clip'}) "
                     f"+ hard-way head over (b t)={B * args.frames} rows + CE + Adam")
     else:
         model = AVENet(orc.Args(), False).to(dev).train()
-        x1, x2 = synthetic_inputs(B, dev, seed=1000 + rank)
+        inputs = synthetic_inputs(B, dev, seed=1000 + rank)
         workload = "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam"
-    step = HardWayTrainStep(model, lr=1e-6, weight_decay=1e-4)
+    if twoview:
+        step = TwoViewTrainStep(model, lr=4e-6, weight_decay=1e-4, dedup_audio=not args.twoview_folded)
+    else:
+        step = HardWayTrainStep(model, lr=1e-6, weight_decay=1e-4)
 
     use_graph = not args.no_graph
     for i in range(max(args.warmup, 1 if use_graph else 0)):
-        loss = step.step(x1, x2)
+        loss = step.step(*inputs)
         if use_graph and i == 0:
-            step.capture(x1, x2)  # later warm-up and all timed steps are graph replays
+            step.capture(*inputs)  # later warm-up and all timed steps are graph replays
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step.step(x1, x2)
+        loss = step.step(*inputs)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    loss_v = float(loss)
+    loss_v = float(loss.flatten()[0])  # twoview: losses[0] = the combined loss
     # roofline of the conv family: HIP events on the launch stream around every conv launch of a
     # few eager steps of the same workload (kept out of the timed region above)
-    eager = HardWayTrainStep.__new__(HardWayTrainStep)
+    eager = type(step).__new__(type(step))
     eager.__dict__.update(step.__dict__)
     eager._graph = None
     with ConvProfiler() as prof:
         for _ in range(args.prof_steps):
-            eager.step(x1, x2)
+            eager.step(*inputs)
         torch.cuda.synchronize()
     conv = prof.summary()
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
