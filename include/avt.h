@@ -32,6 +32,8 @@
  *                                nn.MSELoss(weighted, weighted2), PropagationLoss x2 (losses.py:16-23)
  *   avt_propagation_loss         PropagationLoss.forward (losses.py:22-23) + its gradient
  *   avt_ncthw_to_nhwc_bf16       einops 'b c t h w -> (b t) c h w' of the frames (train_hardway.py:130-131)
+ *   avt_localize_ciou,           the test loops' heatmap -> cIoU protocol (train_hardway_1frame.py:195-206,
+ *   avt_pair_ciou                utils.Evaluator.cal_CIOU utils.py:209-214, utils.mTC 311-318)
  */
 #ifndef AVT_H_
 #define AVT_H_
@@ -173,6 +175,15 @@ int avt_twoview_loss(const float* ce1, const float* ce2, const float* wA1, const
                      float loss_weight, float* out, float* dwA1, float* dwA2, void* stream);
 /* PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (or NULL) = d(loss)/dx */
 int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
+
+/* ---- localisation metrics (test loops of train_hardway*.py / test.py; utils.py:203-239, 311-318) ---- */
+/* A [N][h][w] heatmaps -> cv2 INTER_LINEAR resize to S x S, normalize_img(-.), 1 - ., median
+ * binarisation, cIoU(., gt, 0.5): out [N][3] fp64 = (cIoU, intersection, denominator) when gt
+ * [N][S][S] is given; pred_out [N][S][S] u8 binary maps (either may be NULL, not both) */
+int avt_localize_ciou(const float* A, int N, int h, int w, int S, const float* gt, double* out, void* pred_out,
+                      void* stream);
+/* out[k] = cIoU(p[k], p[k+1], 0.5) of binary maps p [N][n] u8, k < N-1 (utils.mTC) */
+int avt_pair_ciou(const void* p, int N, int n, double* out, void* stream);
 
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
