@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libavt.so")
 # A/B measurement only: load another in-tree build of the same ABI (e.g. libavt_base.so)
 LOAD_PATH = os.environ.get("AVT_LIB_PATH", LIB_PATH)
-SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip", "tube.hip", "eval.hip"]
+SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip", "tube.hip", "eval.hip", "audio.hip"]
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -67,6 +67,8 @@ SIGNATURES = {
     "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "avt_localize_ciou": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "avt_pair_ciou": (_I, [_P, _I, _I, _P, _P]),
+    "avt_spectrogram_segments": (_I, [_L, _I]),
+    "avt_spectrogram": (_I, [_P, _I, _L, _I, _F, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
     "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

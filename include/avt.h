@@ -34,6 +34,8 @@
  *   avt_ncthw_to_nhwc_bf16       einops 'b c t h w -> (b t) c h w' of the frames (train_hardway.py:130-131)
  *   avt_localize_ciou,           the test loops' heatmap -> cIoU protocol (train_hardway_1frame.py:195-206,
  *   avt_pair_ciou                utils.Evaluator.cal_CIOU utils.py:209-214, utils.mTC 311-318)
+ *   avt_spectrogram              the dataset's scipy.signal.spectrogram + log + Normalize(0, 12)
+ *                                (datasets/dataloader.py:86-96, 252-274)
  */
 #ifndef AVT_H_
 #define AVT_H_
@@ -184,6 +186,13 @@ int avt_localize_ciou(const float* A, int N, int h, int w, int S, const float* g
                       void* stream);
 /* out[k] = cIoU(p[k], p[k+1], 0.5) of binary maps p [N][n] u8, k < N-1 (utils.mTC) */
 int avt_pair_ciou(const void* p, int N, int n, double* out, void* stream);
+
+/* ---- audio front end (datasets/dataloader.py:86-96): waveform -> normalised log-spectrogram ---- */
+/* segments of a length-N waveform at hop = nperseg - noverlap (the reference: 512 - 1) */
+int avt_spectrogram_segments(long long n_samples, int hop);
+/* x [B][N] fp32 -> out [B][1][257][nseg] = log(PSD + 1e-7) / 12 with scipy.signal.spectrogram's
+ * defaults (periodic Tukey(0.25), constant detrend, one-sided density scaling), input clipped to [-1,1] */
+int avt_spectrogram(const float* x, int B, long long N, int hop, float fs, float* out, void* stream);
 
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
