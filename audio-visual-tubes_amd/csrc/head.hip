@@ -409,6 +409,11 @@ __global__ __launch_bounds__(1024) void propagation_loss_kernel(const float* __r
   if (threadIdx.x == 0) *loss = a * k;
 }
 
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0.f;
+}
+
 template <typename TA, typename TB>
 static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak, const TB* b, long long sbk,
                   long long sbn, const float* rowscale, const float* kscale, float* c, long long ldc, int splits,
@@ -476,7 +481,9 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
   // the tube head, whose video features come from a detached forward hook, model.py:12-15)
   if (gv != nullptr) sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
   // gan[j][c] (+)= sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
-  if (!gan_accumulate) (void)hipMemsetAsync(gan, 0, (size_t)B * C * sizeof(float), st);
+  // zeroed by a kernel, not hipMemsetAsync: a memset node in a replayed segment graph was observed to
+  // race the kernel after it (tools/diag_seg2.py: garbage gan in ~half of the replays)
+  if (!gan_accumulate) hipLaunchKernelGGL(zero_f32_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, gan, B * C);
   int splits = rows / 256;
   if (splits < 1) splits = 1;
   if (splits > 64) splits = 64;

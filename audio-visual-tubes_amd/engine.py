@@ -9,6 +9,8 @@ Data flow of one 1-frame step (model.py:112-154, train_hardway_1frame.py:129-134
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Tuple
 
@@ -187,6 +189,32 @@ class AVEngine:
         self.stat_views: Dict = {}
         self._stat_arena = None
         self._alloc(flat.flat.device)
+        # run the audio trunk on a second HIP stream, concurrently with the vision trunk (forward and
+        # backward): the two trunks are independent until the head, and their kernels fill each
+        # other's wave-quantisation tails.  The fused step turns it off for world > 1 (the bucketed
+        # all-reduce orders its collectives on one stream).
+        self.concurrent = os.environ.get("AVT_CONCURRENT", "1") != "0"
+        self._side = None
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.flat.flat.device)
+        return self._side
+
+    @contextlib.contextmanager
+    def _branch(self, enabled: bool = True):
+        """Run the body on the side stream, forked from the current one; join() must follow."""
+        if not (self.concurrent and enabled):
+            yield
+            return
+        side = self._side_stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            yield
+
+    def _join(self, enabled: bool = True):
+        if self.concurrent and enabled and self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
 
     def _setup_trunks(self):
         self.img = Trunk("imgnet.", "vision")
@@ -257,17 +285,30 @@ class AVEngine:
         if training:
             self.flat.nbt.add_(1)
             self._stat_arena.zero_()  # accumulators are re-zeroed by their finalize; this is belt and braces
-        xi = self._to_nhwc(image, 4)
-        xa = self._to_nhwc(audio, 1)
-        v, tape_i = self.img.forward(xi, self.store, training)
-        a, tape_a = self.aud.forward(xa, self.store, training)
         dev = image.device
+
+        def audio_branch():
+            xa = self._to_nhwc(audio, 1)
+            a, tape_a = self.aud.forward(xa, self.store, training)
+            C = a.shape[-1]
+            an = torch.empty(B, C, device=dev, dtype=torch.float32)
+            amax = torch.empty(B, C, device=dev, dtype=torch.int32)
+            anorm = torch.empty(B, device=dev, dtype=torch.float32)
+            call("avt_audio_pool_norm_fwd", P(a), P(an), P(amax), P(anorm), B, a.shape[1] * a.shape[2], C,
+                 stream_ptr())
+            return a, tape_a, an, amax, anorm
+
+        if self.concurrent:
+            with self._branch():  # audio trunk (side stream) || vision trunk (current stream)
+                a, tape_a, an, amax, anorm = audio_branch()
+        xi = self._to_nhwc(image, 4)
+        v, tape_i = self.img.forward(xi, self.store, training)
+        if self.concurrent:
+            self._join()
+        else:
+            a, tape_a, an, amax, anorm = audio_branch()
         _, h, w, C = v.shape
         Pn = h * w
-        an = torch.empty(B, C, device=dev, dtype=torch.float32)
-        amax = torch.empty(B, C, device=dev, dtype=torch.int32)
-        anorm = torch.empty(B, device=dev, dtype=torch.float32)
-        call("avt_audio_pool_norm_fwd", P(a), P(an), P(amax), P(anorm), B, a.shape[1] * a.shape[2], C, stream_ptr())
         L = B + (2 if self.neg else 1)
         f32 = dict(device=dev, dtype=torch.float32)
         inv = torch.empty(B, Pn, **f32)
@@ -351,16 +392,21 @@ class AVEngine:
         B, C = tape["B"], tape["C"]
         gv, gan = self.head_backward(tape, dlogits, dwA)
         a = tape["a"]
-        ga = torch.empty_like(a)
-        call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
-             a.shape[1] * a.shape[2], C, stream_ptr())
         self.store.grads = self.flat.grad_views(gflat)
+        par = on_boundary is None  # bucket hooks need the trunks in order on one stream
         try:
+            with self._branch(par):  # audio backward (side stream) || vision backward
+                ga = torch.empty_like(a)
+                call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
+                     a.shape[1] * a.shape[2], C, stream_ptr())
+                if par:
+                    self.aud.backward(tape["aud"], ga, self.store, None)
             self.img.backward(tape["img"], gv, self.store, on_boundary)
             if on_boundary is not None:
                 on_boundary(self.img.prefix + "lo")
-            self.aud.backward(tape["aud"], ga, self.store, on_boundary)
-            if on_boundary is not None:
+            if not par:
+                self.aud.backward(tape["aud"], ga, self.store, on_boundary)
                 on_boundary(self.aud.prefix + "lo")
+            self._join(par)
         finally:
             self.store.grads = None

@@ -58,6 +58,8 @@ class HardWayTrainStep:
         self.pg = process_group
         self.world = world_size(process_group)
         if self.world > 1:
+            self.engine.concurrent = False  # the bucketed all-reduce follows the trunks on one stream
+        if self.world > 1:
             # start from identical weights everywhere (DDP constructor semantics)
             dist.broadcast(self.flat.flat, 0, group=self.pg)
             sync_buffers(self.flat.bflat, self.pg)

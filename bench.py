@@ -225,10 +225,13 @@ def main():
     eager = type(step).__new__(type(step))
     eager.__dict__.update(step.__dict__)
     eager._graph = None
+    conc = step.engine.concurrent
+    step.engine.concurrent = False  # per-kernel durations of the conv launches, not of overlapped pairs
     with ConvProfiler() as prof:
         for _ in range(args.prof_steps):
             eager.step(*inputs)
         torch.cuda.synchronize()
+    step.engine.concurrent = conc
     conv = prof.summary()
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
@@ -274,7 +277,8 @@ def main():
                          "conv_ms_per_step": round(ms / ps, 3),
                          "measured": f"HIP events around each conv launch, {args.prof_steps} eager steps after the "
                                      "timed region"},
-            "launch": "eager" if args.no_graph else "hip-graph replay",
+            "launch": ("eager" if args.no_graph else "hip-graph replay") + (
+                ", audio trunk on a second stream" if step.engine.concurrent else ""),
             # whole step: algorithmic conv FLOPs of one step / step time (head, BN, Adam: < 1 %)
             "step_conv_tflop": round(conv_tflop_step, 4),
             "step_tflops_per_gpu": round(conv_tflop_step / (ms_step * 1e-3), 2),

@@ -119,3 +119,19 @@ def test_two_rank_bucketed_allreduce_matches_dp_mean():
     print(f"max |param(2 ranks) - param(DP reference)| = {d:.3e}")
     # each Adam step moves a weight by <= ~lr; split-K atomics may flip a ~0 gradient's update
     assert d <= (STEPS_EAGER + STEPS_GRAPH) * 2.1e-6, d
+
+
+def test_segment_graph_replay_matches_eager():
+    """The world > 1 capture (one HIP graph per gradient bucket) replays to the eager gradient.
+    Regression: a hipMemsetAsync node in the head backward raced the next kernel in segment
+    replays, leaving garbage audio gradients in about half of the runs (tools/diag_seg2.py)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from diag_seg2 import seg_vs_eager
+
+    for _ in range(3):
+        rel = seg_vs_eager()
+        print(rel)
+        assert all(v < 1e-5 for v in rel.values()), rel
