@@ -44,7 +44,7 @@ def _model(dev):
     return m.to(dev).train()
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, out_q, overlap):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -55,24 +55,28 @@ def _worker(rank, world, port, out_q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         m = _model(dev)
-        step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
+        step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4, overlap_allreduce=overlap)
         img, aud = (t.to(dev) for t in _shards()[rank])
         losses = [step.step(img, aud).item() for _ in range(STEPS_EAGER)]
         step.capture(img.clone(), aud.clone())
         losses += [step.step(img, aud).item() for _ in range(STEPS_GRAPH)]
         torch.cuda.synchronize()
-        out_q.put((rank, np.array(losses), m._flat.flat.cpu().numpy().copy(), len(step._seg_graphs)))
+        nseg = len(step._seg_graphs) if step._seg_graphs is not None else 0
+        out_q.put((rank, np.array(losses), m._flat.flat.cpu().numpy().copy(), nseg))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_bucketed_allreduce_matches_dp_mean():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_two_rank_allreduce_matches_dp_mean(overlap):
+    """overlap=False (default): concurrent-trunk graph + one all-reduce; True: bucketed all-reduces
+    overlapped with a sequential backward (segment graphs)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -93,7 +97,7 @@ def test_two_rank_bucketed_allreduce_matches_dp_mean():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][2] == 4  # imgnet hi/lo, audnet hi/lo segment graphs
+    assert res[0][2] == (4 if overlap else 0)  # imgnet hi/lo, audnet hi/lo segment graphs
     # both ranks hold the same weights
     assert np.abs(res[0][1] - res[1][1]).max() == 0.0
 

@@ -22,7 +22,7 @@ def seg_vs_eager(B=2, seed=0):
     m.load_state_dict(orc.make_state(seed))
     m = m.to(dev).train()
     step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
-    step.world = 2  # take the segmented-capture path; collectives are no-ops
+    step.world, step.overlap = 2, True  # take the segmented-capture path; collectives are no-ops
     step.engine.concurrent = False
     step._allreduce_bucket = lambda tag, works: None
     img, aud = orc.make_image(B, 64).to(dev), orc.make_spectrogram(B, 65, 76).to(dev)
