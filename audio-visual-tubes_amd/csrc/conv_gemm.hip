@@ -459,6 +459,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_nt_pipe.h"
 #include "conv_tn_pipe.h"
 #include "conv_halo.h"
+#include "conv_wgrad_halo.h"
 
 static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
 static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
@@ -467,6 +468,9 @@ static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = 1;        // allow the 8-wave 256-wide wgrad tiles
+static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
+                                   // measured 230-320 TFLOP/s vs 450-820 for the tap-gather kernel, see
+                                   // conv_wgrad_halo.h)
 static int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -919,8 +923,115 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
   }
 }
 
+// ---- halo wgrad plan (conv_wgrad_halo.h) ----
+static int wgrad_halo_enabled() {
+  if (g_wgrad_halo < 0) {
+    const char* e = getenv("AVT_WGRAD_HALO");
+    g_wgrad_halo = e ? atoi(e) : 0;
+  }
+  return g_wgrad_halo;
+}
+
+struct WgradHaloPlan {
+  bool ok;
+  int WM;  // 2: BM 128 (4 waves), 1: BM 64 (2 waves); one wave per SIMD
+  WgradHaloArgs a;
+  size_t slab_bytes;
+  int groups, per_group;  // reduce: split groups
+};
+
+static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
+  WgradHaloPlan pl{};
+  pl.ok = false;
+  if (!wgrad_halo_enabled() || R != 3 || S != 3 || stride != 1 || pad != 1 || Cp != Creal || Cp % 64 != 0 ||
+      K % 64 != 0 || conv_variant() != 1)
+    return pl;
+  WgradHaloArgs& a = pl.a;
+  a.N = N; a.H = H; a.W = W; a.C = Cp; a.K = K;
+  pl.WM = (K % 128 == 0) ? 2 : 1;
+  const int BM = pl.WM * 64;
+  const int PRMAX = pl.WM == 2 ? 160 : 72;
+  const int per_cu = pl.WM == 2 ? 1 : 2;  // resident blocks: one wave per SIMD (288 accumulator registers)
+  // cost of a k-tile: MFMA cycles of a block (4 SIMDs) vs its share of the ~29 B/clk L2->LDS fill
+  const double t_mfma = 2.0 * 32 * BM * 576 / (4 * 1024.0);
+  auto cost = [&](long long tiles, int pr) {
+    const double fill = (32.0 * BM * 2 + pr * 128.0) / (29.0 / per_cu);
+    return (double)tiles * (t_mfma > fill ? t_mfma : fill);
+  };
+  double best = -1;
+  // raster: 32 consecutive pixels span at most ceil(31/W)+1 rows
+  {
+    const int span = (W >= 32 ? 2 : (31 + W - 1) / W + 1);
+    const int pr = (span + 2) * (W + 2);
+    if (pr <= PRMAX) {
+      const long long tiles = (long long)(H * W + 31) / 32;
+      best = cost(tiles, pr);
+      a.raster = 1; a.R = 1; a.CW = 32; a.lcw = 5; a.wcols = 1; a.tiles_img = (int)tiles; a.PW = W + 2; a.PR = pr;
+    }
+  }
+  const int shapes[4][2] = {{1, 32}, {2, 16}, {4, 8}, {8, 4}};
+  for (auto& sh : shapes) {
+    const int r = sh[0], cw = sh[1];
+    const int pr = (r + 2) * (cw + 2);
+    if (pr > PRMAX) continue;
+    const int bands = (H + r - 1) / r, wcols = (W + cw - 1) / cw;
+    const double c = cost((long long)bands * wcols, pr);
+    if (best < 0 || c < best * 0.999) {
+      best = c;
+      a.raster = 0; a.R = r; a.CW = cw; a.lcw = 31 - __builtin_clz(cw); a.wcols = wcols; a.tiles_img = bands * wcols;
+      a.PW = cw + 2; a.PR = pr;
+    }
+  }
+  if (best < 0) return pl;
+  a.nkt = N * a.tiles_img;
+  const int per_split = (K / BM) * (Cp / 64);
+  const long long slots = (long long)num_cus() * per_cu;
+  int splits = (int)(slots / per_split);
+  if (splits < 1) splits = 1;
+  if (splits > a.nkt) splits = a.nkt;
+  const int kps = (a.nkt + splits - 1) / splits;
+  a.kt_per_split = kps;
+  a.splits = (a.nkt + kps - 1) / kps;  // every split non-empty
+  a.div_w = make_magic((unsigned)W);
+  a.div_tiles = make_magic((unsigned)a.tiles_img);
+  a.dy_bytes = (unsigned)((size_t)N * H * W * K * 2);
+  a.x_bytes = (unsigned)((size_t)N * H * W * Cp * 2);
+  pl.slab_bytes = a.splits > 1 ? (size_t)a.splits * K * 9 * Cp * sizeof(float) : 0;
+  pl.per_group = 32;
+  pl.groups = (a.splits + pl.per_group - 1) / pl.per_group;
+  pl.ok = true;
+  return pl;
+}
+
+static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* dy, float* dw, float* slab,
+                              hipStream_t st) {
+  WgradHaloArgs& a = pl.a;
+  a.x = x;
+  a.dy = dy;
+  a.dw = dw;
+  a.slab = slab;
+  const int BM = pl.WM * 64;
+  const int grid = (a.K / BM) * (a.C / 64) * a.splits;
+  if (pl.WM == 2)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 5, 160>), dim3(grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 6, 72>), dim3(grid), dim3(128), 0, st, a);
+  if (slab) {
+    const long long n = (long long)a.K * 9 * a.C;
+    dim3 rg((unsigned)((n / 4 + 255) / 256), (unsigned)pl.groups);
+    hipLaunchKernelGGL(wgrad_halo_reduce_kernel, rg, dim3(256), 0, st, slab, a.splits, pl.per_group, n, dw);
+  }
+}
+
+extern "C" int avt_set_wgrad_halo(int on) {
+  avt::g_wgrad_halo = on ? 1 : 0;
+  return AVT_OK;
+}
+
 extern "C" size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride,
                                              int pad) {
+  const WgradHaloPlan hp = wgrad_halo_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  if (hp.ok) return hp.slab_bytes;
   return wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad).slab_bytes;
 }
 
@@ -935,6 +1046,13 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
   AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
   AVT_REQUIRE(Creal <= Cp, "conv2d_wgrad: Creal > Cp");
   AVT_REQUIRE(Cp % 8 != 0 || Creal == Cp, "conv2d_wgrad: channel padding only for the stems");
+  WgradHaloPlan hp = wgrad_halo_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  if (hp.ok) {
+    // without the workspace the split partials are added with fp32 atomics
+    float* hslab = (hp.slab_bytes > 0 && workspace != nullptr && ws_bytes >= hp.slab_bytes) ? (float*)workspace : nullptr;
+    launch_wgrad_halo(hp, (const bf16_t*)x, (const bf16_t*)dy, dw, hslab, (hipStream_t)stream);
+    return check_launch("conv2d_wgrad(halo)");
+  }
   WgradPlan pl = wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
   pl.p.dy = (const bf16_t*)dy;
   pl.p.x = (const bf16_t*)x;

@@ -83,6 +83,8 @@ int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 /* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
 int avt_set_wgrad_tiles(int big);
+/* 3x3/s1 wgrads on the halo-reuse kernel (1, default; env AVT_WGRAD_HALO) or the tap-gather one (0) */
+int avt_set_wgrad_halo(int on);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);

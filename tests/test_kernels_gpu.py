@@ -260,20 +260,24 @@ def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
          S())
 
 
-@pytest.mark.parametrize("big", [1, 0])
+@pytest.mark.parametrize("big", [1, 0, "halo"])
 @pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_wgrad(case, slab, big):
+    """big: the 256-wide tap-gather tiles (1), 128-wide only (0), or the halo-reuse kernel for the
+    3x3/s1 cases ("halo", off by default; conv_wgrad_halo.h)."""
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
     dy = _rand_act(N, Pq, Qq, K, 9)
     dw = torch.full((K, R, R, C), 0.25, device=DEV)  # accumulates into an existing gradient
     try:
-        call("avt_set_wgrad_tiles", big)
+        call("avt_set_wgrad_tiles", 1 if big == "halo" else big)
+        call("avt_set_wgrad_halo", int(big == "halo"))
         wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
     finally:
         call("avt_set_wgrad_tiles", 1)
+        call("avt_set_wgrad_halo", 0)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()

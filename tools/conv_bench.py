@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
+    ap.add_argument("--wgrad-halo", default="1", help="comma list of avt_set_wgrad_halo values to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -121,7 +122,9 @@ def main():
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
                 tot[("dgrad", v)] = tot.get(("dgrad", v), 0) + ms
             if "wgrad" in kinds and v == 1:
-                for big in [int(t) for t in args.wgrad_tiles.split(",")]:
+                for hv, big in [(int(h), int(t)) for h in args.wgrad_halo.split(",")
+                                for t in args.wgrad_tiles.split(",")]:
+                    call("avt_set_wgrad_halo", hv)
                     call("avt_set_wgrad_tiles", big)
                     for pol in args.wgrad_policy.split(";"):
                         tb, mk = (int(s) for s in pol.split(","))
@@ -130,11 +133,12 @@ def main():
                         ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
                         ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st,
                                                  pad, P(ws), wsb if args.slab else 0, S()))
-                        line += f" wgrad[t{big},{tb},{mk}] {flops / ms / 1e9:6.0f}"
-                        key = f"wgrad_t{big}_{pol}"
+                        line += f" wgrad[h{hv},t{big},{tb},{mk}] {flops / ms / 1e9:6.0f}"
+                        key = f"wgrad_h{hv}_t{big}_{pol}"
                         tot[(key, v)] = tot.get((key, v), 0) + ms
                 call("avt_set_wgrad_policy", 0, 4)
                 call("avt_set_wgrad_tiles", 1)
+                call("avt_set_wgrad_halo", 1)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
