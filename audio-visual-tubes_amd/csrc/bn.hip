@@ -154,26 +154,41 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   }
   const long long rbeg = (long long)blockIdx.x * rows_per_block;
   const long long rend = min(rows, rbeg + rows_per_block);
-  // two rows per iteration: four independent 16-B loads in flight per thread
+  // four rows per iteration: 8-12 independent 16-B loads in flight per thread (HBM-bound: the
+  // bytes in flight per CU set the achieved bandwidth); the remaining rows one at a time
   long long r = rbeg + r0;
-  for (; r + rstep < rend; r += 2 * rstep) {
-    const size_t o0 = (size_t)r * cv + chunk, o1 = o0 + (size_t)rstep * cv;
-    const u32x4 ga = reinterpret_cast<const u32x4*>(g)[o0], gb = reinterpret_cast<const u32x4*>(g)[o1];
-    const u32x4 xa = reinterpret_cast<const u32x4*>(xc)[o0], xb = reinterpret_cast<const u32x4*>(xc)[o1];
-    float g0[8], x0[8], g1[8], x1[8];
-    unpack8(ga, g0);
-    unpack8(xa, x0);
-    unpack8(gb, g1);
-    unpack8(xb, x1);
-    relu_mask8(g0, x0, y, o0, mscale, mshift, c0);
-    relu_mask8(g1, x1, y, o1, mscale, mshift, c0);
+  constexpr int U = 4;
+  for (; r + (U - 1) * rstep < rend; r += U * rstep) {
+    u32x4 gq[U], xq[U], yq[U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += g0[e] + g1[e];
-      s2[e] += g0[e] * (x0[e] - mu[e]) * is[e] + g1[e] * (x1[e] - mu[e]) * is[e];
+    for (int u = 0; u < U; ++u) {
+      const size_t o = (size_t)(r + u * rstep) * cv + chunk;
+      gq[u] = reinterpret_cast<const u32x4*>(g)[o];
+      xq[u] = reinterpret_cast<const u32x4*>(xc)[o];
+      if (y) yq[u] = reinterpret_cast<const u32x4*>(y)[o];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float gg[8], xx[8];
+      unpack8(gq[u], gg);
+      unpack8(xq[u], xx);
+      if (y) {
+        float yy[8];
+        unpack8(yq[u], yy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gg[e] = yy[e] > 0.f ? gg[e] : 0.f;
+      } else if (mscale) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gg[e] = __builtin_fmaf(xx[e], mscale[c0 + e], mshift[c0 + e]) > 0.f ? gg[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += gg[e];
+        s2[e] += gg[e] * (xx[e] - mu[e]) * is[e];
+      }
     }
   }
-  if (r < rend) {
+  for (; r < rend; r += rstep) {
     const size_t off = (size_t)r * cv + chunk;
     float gg[8], xx[8];
     unpack8(reinterpret_cast<const u32x4*>(g)[off], gg);
