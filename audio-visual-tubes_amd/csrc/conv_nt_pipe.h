@@ -28,8 +28,20 @@ constexpr unsigned kOOB = 0x80000000u;  // beyond any activation buffer: the loa
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// Issued as inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: the compiler treats every
+// LDS read after a builtin LDS-DMA as possibly aliasing it and inserts `s_waitcnt vmcnt(0)` in
+// front of the fragment reads, which drains ALL in-flight tiles each k-step and collapses the
+// NST-stage ring to no overlap at all (seen in the gfx950 assembly of the TN and halo kernels).
+// Opaque to the waitcnt pass, the loads are ordered only by the kernels' own counted
+// wait_vmcnt + s_barrier, which is what the ring was designed around.  (vmcnt retires in issue
+// order, so the compiler's waits for its own loads stay correct — at worst they over-wait.)
+// m0 carries the wave's LDS base.  It is not listed as clobbered: LLVM ignores clobbers of reserved
+// registers (with a warning per instantiation); the gfx950 code of these kernels has no other m0
+// use (no movrel/sendmsg; checked in the --save-temps assembly), so nothing live is overwritten.
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds_wave_base, 16, voff, 0, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(rs)
+               : "memory");
 }
 
 constexpr int kMaxTaps = 49;  // 7x7 (the R3D stem as a 32-channel Conv2d); 3x3x3 Conv3d needs 27
