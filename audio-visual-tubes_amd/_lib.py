@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libavt.so")
 # A/B measurement only: load another in-tree build of the same ABI (e.g. libavt_base.so)
 LOAD_PATH = os.environ.get("AVT_LIB_PATH", LIB_PATH)
-SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip", "tube.hip", "eval.hip", "audio.hip"]
+SOURCES = ["conv_gemm.hip", "bn.hip", "pool.hip", "head.hip", "misc.hip", "tube.hip", "eval.hip", "audio.hip", "frames.hip"]
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -33,6 +33,7 @@ SIGNATURES = {
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
+    "avt_set_stem_kernel": (_I, [_I]),
     "avt_set_nt128_config": (_I, [_I]),
     "avt_set_wgrad_slab_max": (_I, [_I, _I]),
     "avt_set_wgrad_tiles": (_I, [_I]),
@@ -70,6 +71,7 @@ SIGNATURES = {
     "avt_pair_ciou": (_I, [_P, _I, _I, _P, _P]),
     "avt_spectrogram_segments": (_I, [_L, _I]),
     "avt_spectrogram": (_I, [_P, _I, _L, _I, _F, _P, _P]),
+    "avt_frames_transform": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
     "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -460,6 +460,17 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_tn_pipe.h"
 #include "conv_halo.h"
 #include "conv_wgrad_halo.h"
+#include "conv_stem.h"
+
+static int g_stem_kernel = -1;  // 7x7/s2 stems on conv_stem_fwd_kernel: -1 = env AVT_STEM (default 0, the
+                                // generic gather kernel: measured 0.25 ms/step faster at B=128, conv_stem.h)
+static int stem_enabled() {
+  if (g_stem_kernel < 0) {
+    const char* e = getenv("AVT_STEM");
+    g_stem_kernel = e ? atoi(e) : 0;
+  }
+  return g_stem_kernel;
+}
 
 static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
 static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
@@ -536,6 +547,11 @@ extern "C" int avt_set_wgrad_slab_max(int max_splits, int wave_cost) {
   AVT_REQUIRE(max_splits >= 0 && wave_cost >= 0, "set_wgrad_slab_max: bad arguments");
   avt::g_wgrad_slab_max = max_splits;
   avt::g_wgrad_wave_cost = wave_cost;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_stem_kernel(int on) {
+  avt::g_stem_kernel = on ? 1 : 0;
   return AVT_OK;
 }
 
@@ -729,6 +745,22 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   p.Kg = Kg;
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
   hipStream_t st = (hipStream_t)stream;
+  if ((Cp == 4 || Cp == 1) && stem_enabled() && K == 64 && R == 7 && S == 7 && stride == 2 && pad == 3 &&
+      (Cp == 4 ? stem_fits<4>(p.OW) : stem_fits<1>(p.OW))) {
+    StemArgs sa{};
+    sa.x = p.act;
+    sa.w = p.wmat;
+    sa.y = p.out;
+    sa.stats = bn_acc;
+    sa.IH = H; sa.IW = W; sa.OH = p.OH; sa.OW = p.OW; sa.Kg = Kg;
+    sa.blocks_per_img = (p.OH * p.OW + kStemBM - 1) / kStemBM;
+    const dim3 grid(N * sa.blocks_per_img);
+    if (Cp == 4)
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<4>, grid, dim3(256), 0, st, sa);
+    else
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<1>, grid, dim3(256), 0, st, sa);
+    return check_launch("conv2d_fwd (stem)");
+  }
   const bool bn128 = (K % 128 == 0);
   if (Cp == 4) {
     launch_nt<MODE_FWD, 4, 128, 64>(p, st);

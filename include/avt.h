@@ -35,6 +35,8 @@
  *   avt_localize_ciou,           the test loops' heatmap -> cIoU protocol (train_hardway_1frame.py:195-206,
  *   avt_pair_ciou                utils.Evaluator.cal_CIOU utils.py:209-214, utils.mTC 311-318)
  *   avt_spectrogram              the dataset's scipy.signal.spectrogram + log + Normalize(0, 12)
+ *   avt_frames_transform         the dataset's frame transform: PIL BICUBIC Resize + crop + flip + ToTensor +
+ *                                Normalize (datasets/dataloader.py:47-62)
  *                                (datasets/dataloader.py:86-96, 252-274)
  */
 #ifndef AVT_H_
@@ -83,8 +85,11 @@ int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 /* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
 int avt_set_wgrad_tiles(int big);
-/* 3x3/s1 wgrads on the halo-reuse kernel (1, default; env AVT_WGRAD_HALO) or the tap-gather one (0) */
+/* 3x3/s1 wgrads on the halo-reuse kernel (1; env AVT_WGRAD_HALO) or the tap-gather one (0, default) */
 int avt_set_wgrad_halo(int on);
+/* 1: the 7x7/s2 stems (C 4 or 1, K 64) run on the LDS-patch stem kernel; 0 (default, env AVT_STEM):
+ * the generic gather kernel, measured faster in the B=128 step — an A/B knob */
+int avt_set_stem_kernel(int on);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);
@@ -195,6 +200,14 @@ int avt_spectrogram_segments(long long n_samples, int hop);
 /* x [B][N] fp32 -> out [B][1][257][nseg] = log(PSD + 1e-7) / 12 with scipy.signal.spectrogram's
  * defaults (periodic Tukey(0.25), constant detrend, one-sided density scaling), input clipped to [-1,1] */
 int avt_spectrogram(const float* x, int B, long long N, int hop, float fs, float* out, void* stream);
+
+/* ---- frame transform (datasets/dataloader.py:47-62): decoded RGB frames -> normalised tensors ----
+ * src: uint8 HWC frames packed at byte offsets; desc: DEVICE int64 [n][8] = {offset, H, W, resized_h,
+ * resized_w, crop_top, crop_left, flip}; tmp: device scratch of n*3*Hmax*S bytes; mean/std: HOST
+ * float[3]; out: float32 [n][3][S][S].  The resize is bit-identical to Pillow's Image.resize(BICUBIC)
+ * (fixed-point separable resampler); S <= 256, downscale factor <= 7.5 (checked by the caller). */
+int avt_frames_transform(const void* src, const long long* desc, int n, int S, int Hmax, void* tmp,
+                         const float* mean, const float* std, float* out, void* stream);
 
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,

@@ -216,13 +216,29 @@ def test_stem_fwd_wgrad(cin, cp, H, W):
     wf, _ = pack(w.to(DEV), cp, kg, with_t=False)
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     y = torch.empty(N, Pq, Qq, K, device=DEV, dtype=torch.bfloat16)
-    call("avt_conv2d_fwd", P(xn), P(wf), P(y), None, N, H, W, cp, K, R, R, st, pad, kg, S())
     xb = x.to(torch.bfloat16).double()
     wb = w.to(torch.bfloat16).double().permute(0, 3, 1, 2)
     ref = F.conv2d(xb, wb, stride=st, padding=pad).permute(0, 2, 3, 1)
-    torch.cuda.synchronize()
+    rows = ref.reshape(-1, K)
+    n = rows.shape[0]
+    outs = []
+    try:
+        for stem_kernel in (1, 0):  # the LDS-patch stem kernel and the generic gather kernel (default)
+            call("avt_set_stem_kernel", stem_kernel)
+            acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+            call("avt_conv2d_fwd", P(xn), P(wf), P(y), P(acc), N, H, W, cp, K, R, R, st, pad, kg, S())
+            torch.cuda.synchronize()
+            assert rel_err(y, ref) < 8e-3, stem_kernel
+            a = acc.view(-1, K, 3).sum(0).cpu()
+            np.testing.assert_allclose(a[:, 0].numpy(), rows.sum(0).numpy(), rtol=1e-4,
+                                       atol=1e-4 * rows.abs().max().item() * n ** 0.5)
+            m2 = a[:, 1] + a[:, 2] - a[:, 0] ** 2 / n
+            np.testing.assert_allclose(m2.numpy(), ((rows - rows.mean(0)) ** 2).sum(0).numpy(), rtol=1e-4)
+            outs.append(y.clone())
+    finally:
+        call("avt_set_stem_kernel", 0)
+    assert (outs[0].float() - outs[1].float()).abs().gt(0).float().mean().item() < 0.05
     assert torch.equal(xn[..., :cin].float().cpu(), x.to(torch.bfloat16).permute(0, 2, 3, 1).float())
-    assert rel_err(y, ref) < 8e-3
     dy = _rand_act(N, Pq, Qq, K, 4)
     dw = torch.zeros(K, R, R, cin, device=DEV)
     wgrad(xn, dy.to(DEV), dw, N, H, W, cp, cin, K, R, st, pad)

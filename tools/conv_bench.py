@@ -59,7 +59,8 @@ def main():
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
-    ap.add_argument("--wgrad-halo", default="1", help="comma list of avt_set_wgrad_halo values to sweep")
+    ap.add_argument("--wgrad-halo", default="0", help="comma list of avt_set_wgrad_halo values to sweep")
+    ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -83,6 +84,19 @@ def main():
         acc = torch.zeros(16 * K * 3, device=dev, dtype=torch.float64)
         flops = 2.0 * N * Pq * Qq * K * C * R * R
         line = f"{name:12s} M={N * Pq * Qq:7d} N={K:4d} K={kg:5d}"
+        if args.halo and R == 3 and st == 1:
+            for hv in [int(s) for s in args.halo.split(",")]:
+                call("avt_set_halo", hv)
+                call("avt_set_conv_variant", 1)
+                ms = timeit(lambda: call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad,
+                                         kg, S()))
+                line += f" | halo[{hv}] fwd {flops / ms / 1e9:6.0f}"
+                ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
+                                         pad, S()))
+                line += f" dgrad {flops / ms / 1e9:6.0f}"
+            call("avt_set_halo", 1)
+        if (args.nt64 or args.nt128) and args.halo:
+            call("avt_set_halo", 0)  # the tap-gather configs on every shape
         if args.nt64 and K == 64 or args.nt64 and C == 64:
             for cfg in [int(s) for s in args.nt64.split(",")]:
                 call("avt_set_nt64_config", cfg)
@@ -109,6 +123,7 @@ def main():
                                              pad, S()))
                     line += f" nt128[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
             call("avt_set_nt128_config", -1)
+        call("avt_set_halo", 1)
         for v in [int(s) for s in args.variants.split(",")]:
             call("avt_set_conv_variant", v)
             if "fwd" in kinds:
@@ -138,7 +153,7 @@ def main():
                         tot[(key, v)] = tot.get((key, v), 0) + ms
                 call("avt_set_wgrad_policy", 0, 4)
                 call("avt_set_wgrad_tiles", 1)
-                call("avt_set_wgrad_halo", 1)
+                call("avt_set_wgrad_halo", 0)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
