@@ -19,9 +19,11 @@
 // coalesced stores.  Bound: the 2 B per output element store (205 MB vision, 317 MB audio at
 // B = 128) and the MFMA work of the padded K.
 // Measured on MI355X (tools/stem_ab.sh, B = 128 step): conv fwd 3.42 ms/step here vs 3.16 ms on the
-// generic kernel, so it is OFF by default (AVT_STEM=1 / avt_set_stem_kernel(1) selects it).  Likely
-// causes: one image per block leaves the last block of each image partly idle (OH*OW % 512), and the
-// 8 KB-per-row LDS patch fill is serialised ahead of the MFMA work (no double buffering).
+// generic kernel at 1 wave/SIMD (213 VGPR + 128 AGPR); with __launch_bounds__(256, 2) and the k loop
+// unrolled by 2 (220 VGPR, 2 blocks per CU) 3.35 vs 3.30 ms -- a tie, so it stays OFF by default
+// (AVT_STEM=1 / avt_set_stem_kernel(1) selects it).  What is left: one image per block leaves the
+// last block of each image partly idle (OH*OW % 512), and the LDS patch fill is serialised ahead of
+// the MFMA work (no double buffering) -- the store-bound floor (35-45 us per stem) is ~4x away.
 #pragma once
 
 struct StemArgs {
@@ -45,7 +47,7 @@ struct StemCfg {
 };
 
 template <int C>
-__global__ __launch_bounds__(256) void conv_stem_fwd_kernel(StemArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_stem_fwd_kernel(StemArgs a) {
   using Cfg = StemCfg<C>;
   constexpr int KS = Cfg::KS, BP = Cfg::BP;
   __shared__ __attribute__((aligned(16))) char smem[kStemLds];
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void conv_stem_fwd_kernel(StemArgs a) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-#pragma unroll
+#pragma unroll 2
   for (int ks = 0; ks < KS; ++ks) {
     bf16x8 bfr[2];
 #pragma unroll
