@@ -627,8 +627,10 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
       pc.OH = (p.OH - ph + 1) / 2;
       pc.OW = (p.OW - pw + 1) / 2;
       pc.M = batch * pc.OH * pc.OW;
-      // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) still runs with an
-      // empty K loop: its rows are written as 0 (+ add)
+      // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) runs with an empty
+      // K loop: its rows are written as 0 (+ add) -- or, accumulating in place (add == out), are
+      // already final and are skipped
+      if (tc.ntaps == 0 && p.add != nullptr && p.add == p.out) continue;
       launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
     }
 }
@@ -880,6 +882,11 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   // waves take the largest split count that fits, s_w = floor(w*slots/tiles), and keep the one
   // with the least w * (ceil(nkt/s_w) + wave_cost) -- k-tiles per block plus its fixed
   // prologue/epilogue cost.
+  // 1x1 convs (the downsample shortcuts): a k-tile is only 32 pixels x (BM + BN) operand rows while
+  // the epilogue still writes a BM x BN fp32 tile, so blocks need deeper K ranges than the wave
+  // model picks (measured, tools/conv_bench.py: min 24 k-tiles takes the six downsample wgrads from
+  // 0.239 to 0.143 ms at B = 128; the 3x3 shapes keep their optimum at 4)
+  const int min_kt = (R * S == 1) ? max(g_wgrad_min_kt, 24) : g_wgrad_min_kt;
   int splits;
   if (g_wgrad_blocks > 0) {
     splits = g_wgrad_blocks / pl.tiles;
@@ -893,7 +900,7 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
     for (int w = 1; w <= 4; ++w) {
       const int s_w = (int)(w * slots / pl.tiles);
       if (s_w < 1) continue;
-      const int kps_w = max(g_wgrad_min_kt, (nkt + s_w - 1) / s_w);
+      const int kps_w = max(min_kt, (nkt + s_w - 1) / s_w);
       const long long waves = (((long long)pl.tiles * ((nkt + kps_w - 1) / kps_w)) + slots - 1) / slots;
       const long long cost = waves * (kps_w + g_wgrad_wave_cost);
       if (best < 0 || cost < best) {
@@ -904,7 +911,7 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   }
   if (splits < 1) splits = 1;
   int kps = (nkt + splits - 1) / splits;
-  if (kps < g_wgrad_min_kt) kps = g_wgrad_min_kt;
+  if (kps < min_kt) kps = min_kt;
   pl.splits = (nkt + kps - 1) / kps;
   p.kt_per_split = kps;
   // slab + reduce pass for moderate split counts (measured faster on layer3/4); very deep splits

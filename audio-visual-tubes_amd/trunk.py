@@ -275,9 +275,11 @@ class Trunk:
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
 
-    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None):
+    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False):
+        """inplace: accumulate into `add` (dx = add + dgrad); a strided 1x1 conv then only touches the
+        pixels its taps reach (the other parity classes of avt_conv2d_dgrad are skipped)."""
         _, wt = store.packed(spec)
-        gx = torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
+        gx = add if inplace else torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
         ev = ConvProfiler.begin()
         call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
              spec.stride, spec.pad, stream_ptr())
@@ -309,7 +311,7 @@ class Trunk:
                 g_cd = self._bn_bwd(g, t["out"], t["cd"], t["sd"], blk["bnd"], store)
                 self._wgrad(t["x"], g_cd, N, Hc, Wc, blk["down"], store)
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store)
-                g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x)
+                g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True)
             g = g_x
         # maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)
         H1, W1 = tape["H1"], tape["W1"]

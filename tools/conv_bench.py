@@ -24,6 +24,11 @@ SHAPES = [
     ("A.l3 3x3", 17, 19, 256, 256, 3, 1, 1),
     ("A.l4 3x3", 17, 19, 512, 512, 3, 1, 1),
     ("A.ds 1x1s2", 33, 38, 128, 256, 1, 2, 0),
+    ("V.ds2 1x1s2", 56, 56, 64, 128, 1, 2, 0),
+    ("V.ds3 1x1s2", 28, 28, 128, 256, 1, 2, 0),
+    ("V.ds4 1x1", 14, 14, 256, 512, 1, 1, 0),
+    ("A.ds2 1x1s2", 65, 75, 64, 128, 1, 2, 0),
+    ("A.ds4 1x1", 17, 19, 256, 512, 1, 1, 0),
 ]
 
 
