@@ -39,6 +39,11 @@ __global__ __launch_bounds__(256) void vis_norm_kernel(const bf16_t* __restrict_
 //   A(m,k) = a[m*sam + k*sak] (TA = bf16_t or float), B(k,n) = b[k*sbk + n*sbn] (TB)
 //   split-K over gridDim.z with fp32 atomics when gridDim.z > 1 (C pre-zeroed by caller, or holding
 //   what to add to); accum = 1 adds to C in the single-split case too.
+// 64x64 block tile, 32-deep k-tiles staged through LDS as fp32; four waves each own a 32x32 quarter
+// on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: full fp32 products and fp32 accumulation, as
+// the reference's fp32 einsum -- only the summation order differs), 16 MFMAs per k-tile.  Each
+// thread fetches 8 consecutive elements along an operand's unit-stride dimension (16-B loads where
+// aligned and in bounds), and the next k-tile's loads are issued before the current tile's MFMAs.
 template <typename T>
 __device__ __forceinline__ float ldf(const T* p, size_t i);
 template <>
@@ -46,86 +51,126 @@ __device__ __forceinline__ float ldf<float>(const float* p, size_t i) { return p
 template <>
 __device__ __forceinline__ float ldf<bf16_t>(const bf16_t* p, size_t i) { return bf2f(p[i]); }
 
+// 8 elements p[i], p[i + st], ..., p[i + 7 st] (only the first `n` valid; the rest 0)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, size_t i, long long st, int n, float* o) {
+  const T* q = p + i;
+  if (n >= 8 && st == 1 && ((uintptr_t)q & 15) == 0) {
+    if constexpr (sizeof(T) == 2) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[2 * e] = bf2f((bf16_t)(v[e] & 0xffff));
+        o[2 * e + 1] = bf2f((bf16_t)(v[e] >> 16));
+      }
+    } else {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(q);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(q + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = v0[e];
+        o[4 + e] = v1[e];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = e < n ? ldf<T>(p, i + (size_t)e * st) : 0.f;
+}
+
+constexpr int kSgKT = 32;  // k-tile depth
+
 template <typename TA, typename TB>
 __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const TA* __restrict__ a, long long sam,
                                                     long long sak, const TB* __restrict__ b, long long sbk,
                                                     long long sbn, const float* __restrict__ rowscale,
                                                     const float* __restrict__ kscale, float* __restrict__ c,
                                                     long long ldc, int k_per_split, int accum) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64 + 4];
+  __shared__ __attribute__((aligned(16))) float As[kSgKT][64 + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[kSgKT][64 + 4];
   const int tid = threadIdx.x;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int kbeg = blockIdx.z * k_per_split, kend = min(K, kbeg + k_per_split);
-  const int tm = tid / 16, tn = tid % 16;
-  float acc[4][4];
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;       // this wave's 32x32 quarter
+  const int frow = lane & 31, fk = lane >> 5;  // MFMA operand lane: row/col, k within the pair
+  // per-thread fetch: 8 consecutive elements along the unit-stride dimension (k when sak/sbk == 1,
+  // else m / n), i.e. (row tid/4, k 8*(tid%4)..) or (k tid/8, rows 8*(tid%8)..)
+  const bool a_kf = (sak == 1), b_kf = (sbk == 1);
+  const int a_r = a_kf ? tid >> 2 : (tid & 7) * 8, a_k = a_kf ? (tid & 3) * 8 : tid >> 3;
+  const int b_r = b_kf ? tid >> 2 : (tid & 7) * 8, b_k = b_kf ? (tid & 3) * 8 : tid >> 3;
+  float ra[8], rb[8];
+  auto fetch = [&](int k0) {
+    const int gk = k0 + a_k, gm = m0 + a_r;
+    if (a_kf) {
+      const int n = (gm < M) ? min(8, kend - gk) : 0;
+      ld8<TA>(a, (size_t)gm * sam + gk, 1, n, ra);
+      if (kscale)
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+        for (int e = 0; e < 8; ++e) ra[e] *= (e < n) ? kscale[gk + e] : 0.f;
+    } else {
+      const int n = (gk < kend) ? min(8, M - gm) : 0;
+      ld8<TA>(a, (size_t)gk * sak + (size_t)gm * sam, sam, n, ra);
+      if (kscale && n > 0) {
+        const float ks = kscale[gk];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  const bool a_kfast = (sak == 1), b_nfast = (sbn == 1);
-  for (int k0 = kbeg; k0 < kend; k0 += 16) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + 256 * e;  // 1024 elements of the 64x16 A tile
-      int mm, kk;
-      if (a_kfast) {
-        mm = idx / 16;
-        kk = idx % 16;
-      } else {
-        mm = idx % 64;
-        kk = idx / 64;
+        for (int e = 0; e < 8; ++e) ra[e] *= ks;
       }
-      const int gm = m0 + mm, gk = k0 + kk;
-      float val = 0.f;
-      if (gm < M && gk < kend) {
-        val = ldf<TA>(a, (size_t)gm * sam + (size_t)gk * sak);
-        if (kscale) val *= kscale[gk];
-      }
-      As[kk][mm] = val;
-      int nn;
-      if (b_nfast) {
-        nn = idx % 64;
-        kk = idx / 64;
-      } else {
-        nn = idx / 16;
-        kk = idx % 16;
-      }
-      const int gn = n0 + nn;
-      const int gk2 = k0 + kk;
-      Bs[kk][nn] = (gn < N && gk2 < kend) ? ldf<TB>(b, (size_t)gk2 * sbk + (size_t)gn * sbn) : 0.f;
     }
+    const int gk2 = k0 + b_k, gn = n0 + b_r;
+    if (b_kf) {
+      const int n = (gn < N) ? min(8, kend - gk2) : 0;
+      ld8<TB>(b, (size_t)gn * sbn + gk2, 1, n, rb);
+    } else {
+      const int n = (gk2 < kend) ? min(8, N - gn) : 0;
+      ld8<TB>(b, (size_t)gk2 * sbk + (size_t)gn * sbn, sbn, n, rb);
+    }
+  };
+  auto stash = [&]() {
+    if (a_kf) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) As[a_k + e][a_r] = ra[e];
+    } else {
+      *reinterpret_cast<f32x4*>(&As[a_k][a_r]) = f32x4{ra[0], ra[1], ra[2], ra[3]};
+      *reinterpret_cast<f32x4*>(&As[a_k][a_r + 4]) = f32x4{ra[4], ra[5], ra[6], ra[7]};
+    }
+    if (b_kf) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Bs[b_k + e][b_r] = rb[e];
+    } else {
+      *reinterpret_cast<f32x4*>(&Bs[b_k][b_r]) = f32x4{rb[0], rb[1], rb[2], rb[3]};
+      *reinterpret_cast<f32x4*>(&Bs[b_k][b_r + 4]) = f32x4{rb[4], rb[5], rb[6], rb[7]};
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+  if (kbeg < kend) fetch(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += kSgKT) {
+    stash();
     __syncthreads();
+    if (k0 + kSgKT < kend) fetch(k0 + kSgKT);  // in flight during this tile's MFMAs
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      float av[4], bv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = As[kk][tm * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = Bs[kk][tn + 16 * j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += av[i] * bv[j];
+    for (int kp = 0; kp < kSgKT; kp += 2) {
+      const float av = As[kp + fk][wm * 32 + frow];
+      const float bv = Bs[kp + fk][wn * 32 + frow];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
     __syncthreads();
   }
+  // C layout of a 32x32 MFMA tile: element v of lane l is row (v&3) + 8(v>>2) + 4(l>>5), column l&31
+  const int gn = n0 + wn * 32 + frow;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int gm = m0 + tm * 4 + i;
-    if (gm >= M) continue;
-    const float rs = rowscale ? rowscale[gm] : 1.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gn = n0 + tn + 16 * j;
-      if (gn >= N) continue;
-      if (gridDim.z > 1)
-        atomicAdd(c + (size_t)gm * ldc + gn, acc[i][j] * rs);
-      else if (accum)
-        c[(size_t)gm * ldc + gn] += acc[i][j] * rs;
-      else
-        c[(size_t)gm * ldc + gn] = acc[i][j] * rs;
-    }
+  for (int v = 0; v < 16; ++v) {
+    const int gm = m0 + wm * 32 + (v & 3) + 8 * (v >> 2) + 4 * fk;
+    if (gm >= M || gn >= N) continue;
+    const float r = acc[v] * (rowscale ? rowscale[gm] : 1.f);
+    if (gridDim.z > 1)
+      atomicAdd(c + (size_t)gm * ldc + gn, r);
+    else if (accum)
+      c[(size_t)gm * ldc + gn] += r;
+    else
+      c[(size_t)gm * ldc + gn] = r;
   }
 }
 
@@ -419,7 +464,7 @@ static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak
                   long long sbn, const float* rowscale, const float* kscale, float* c, long long ldc, int splits,
                   hipStream_t st, int accum = 0) {
   int kps = (K + splits - 1) / splits;
-  kps = ((kps + 15) / 16) * 16;
+  kps = ((kps + kSgKT - 1) / kSgKT) * kSgKT;
   splits = (K + kps - 1) / kps;
   dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
   hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
