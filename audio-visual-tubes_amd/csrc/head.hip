@@ -178,30 +178,49 @@ __device__ __forceinline__ float sigm(float z) { return 1.f / (1.f + __expf(-z))
 
 // ---- logits: one block per row i ----
 // save layout (floats per row): [0..B) s_ij, [B..2B) W_ij, 2B: s1, 2B+1: W1, 2B+2: s2, 2B+3: W2
-__global__ __launch_bounds__(256) void hardway_logits_kernel(const float* __restrict__ A0, const float* __restrict__ vsum,
+__global__ __launch_bounds__(1024) void hardway_logits_kernel(const float* __restrict__ A0, const float* __restrict__ vsum,
                                                              const float* __restrict__ inv, int B, int P, int C,
                                                              float eps1, float eps2, float tau, int trimap, int use_neg,
                                                              float* __restrict__ logits, float* __restrict__ Aout,
                                                              float* __restrict__ Pos, float* __restrict__ Neg,
                                                              float* __restrict__ wA, float* __restrict__ save) {
   __shared__ float red[16];
-  const int i = blockIdx.x, tid = threadIdx.x;
+  __shared__ float part_w[1024], part_x[1024];
+  const int i = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
   const int L = B + 1 + (use_neg ? 1 : 0);
   const float* row = A0 + (size_t)i * P * B;
   float* sv = save + (size_t)i * (2 * B + 4);
   const float inv_t = 1.f / tau;
-  for (int j = tid; j < B; j += blockDim.x) {
+  // sim[i, j] over the P positions: the block takes jb = min(B, nthr) columns per pass and splits
+  // each column's P positions over nsub = nthr / jb threads (coalesced over j), then combines the
+  // partial sums through LDS -- B columns x P serial steps would leave most of the chip idle
+  const int jb = min(B, nthr), nsub = nthr / jb;
+  const int jl = tid % jb, part = tid / jb;
+  for (int j0 = 0; j0 < B; j0 += jb) {
+    const int j = j0 + jl;
     float sw = 0.f, swx = 0.f;
-    for (int p = 0; p < P; ++p) {
-      const float x = row[(size_t)p * B + j];
-      const float w = sigm((x - eps1) * inv_t);
-      sw += w;
-      swx += w * x;
+    if (j < B && part < nsub)
+      for (int p = part; p < P; p += nsub) {
+        const float x = row[(size_t)p * B + j];
+        const float w = sigm((x - eps1) * inv_t);
+        sw += w;
+        swx += w * x;
+      }
+    part_w[tid] = sw;
+    part_x[tid] = swx;
+    __syncthreads();
+    if (part == 0 && j < B) {
+      float tw = 0.f, tx = 0.f;
+      for (int k = 0; k < nsub; ++k) {
+        tw += part_w[k * jb + jl];
+        tx += part_x[k * jb + jl];
+      }
+      const float s = tx / tw;
+      sv[j] = s;
+      sv[B + j] = tw;
+      logits[(size_t)i * L + 1 + j] = s * (j == i ? -99.f : 1.f) / 0.07f;
     }
-    const float s = swx / sw;
-    sv[j] = s;
-    sv[B + j] = sw;
-    logits[(size_t)i * L + 1 + j] = s * (j == i ? -99.f : 1.f) / 0.07f;
+    __syncthreads();
   }
   // positive / negative on A = A0[i, :, i]
   float s1w = 0.f, s1x = 0.f, s2w = 0.f, s2x = 0.f, pp = 0.f;
@@ -268,7 +287,7 @@ __global__ __launch_bounds__(1024) void hardway_ce_kernel(const float* __restric
   if (threadIdx.x == 0 && loss) *loss = tot / (float)B;
 }
 
-// ---- backward of the logits w.r.t. A0: one block per row i; dA0 [B][P][B] ----
+// ---- backward of the logits w.r.t. A0: blocks (i, slice of the P*B elements of row i); dA0 [B][P][B] ----
 __global__ __launch_bounds__(256) void hardway_logits_bwd_kernel(const float* __restrict__ A0,
                                                                  const float* __restrict__ save,
                                                                  const float* __restrict__ dlogits, int B, int P,
@@ -285,7 +304,7 @@ __global__ __launch_bounds__(256) void hardway_logits_bwd_kernel(const float* __
   const float ds1 = dl[0] / 0.07f;
   const float ds2 = use_neg ? dl[B + 1] / 0.07f : 0.f;
   const size_t n = (size_t)P * B;
-  for (size_t t = threadIdx.x; t < n; t += blockDim.x) {
+  for (size_t t = (size_t)blockIdx.y * blockDim.x + threadIdx.x; t < n; t += (size_t)gridDim.y * blockDim.x) {
     const int j = (int)(t % B);
     const float x = row[t];
     const float w = sigm((x - eps1) * inv_t);
@@ -491,8 +510,8 @@ extern "C" int avt_hardway_fwd(const void* v, const float* an, int B, int P, int
   hipLaunchKernelGGL(vis_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, vsum, rows, C);
   // A0[(i,p)][j] = inv[(i,p)] * sum_c v[(i,p)][c] * an[j][c]
   sgemm<bf16_t, float>(rows, B, C, (const bf16_t*)v, C, 1, an, 1, C, inv, nullptr, A0, B, 1, st);
-  hipLaunchKernelGGL(hardway_logits_kernel, dim3(B), dim3(256), 0, st, A0, vsum, inv, B, P, C, eps1, eps2, tau, trimap,
-                     use_neg, logits, Aout, Pos, Neg, wA, save);
+  hipLaunchKernelGGL(hardway_logits_kernel, dim3(B), dim3(1024), 0, st, A0, vsum, inv, B, P, C, eps1, eps2, tau,
+                     trimap, use_neg, logits, Aout, Pos, Neg, wA, save);
   return check_launch("hardway_fwd");
 }
 
@@ -518,8 +537,10 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
   AVT_REQUIRE(dwA == nullptr || (vsum && dm && gv), "hardway_bwd: dwA needs vsum, dm and the vision gradient");
   hipStream_t st = (hipStream_t)stream;
   const int rows = B * P;
-  hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2, tau,
-                     trimap, use_neg, dA0);
+  // ~8 elements per thread: B = 128 -> 128 x 12 blocks instead of 128 long-running ones
+  const int nslice = (int)min(64LL, max(1LL, ((long long)P * B + 2047) / 2048));
+  hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B, nslice), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2,
+                     tau, trimap, use_neg, dA0);
   if (dwA != nullptr)
     hipLaunchKernelGGL(hardway_wa_bwd_kernel, dim3(B), dim3(256), 0, st, A0, dwA, vsum, inv, B, P, C, eps1, tau, dA0, dm);
   // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]   (skipped when the vision map is detached:

@@ -104,16 +104,29 @@ __global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(const bf16_t* __res
   }
 }
 
-// One block of 512 threads per sample: thread = (8-channel block cg, row group rg); each thread
-// scans rows rg, rg + RG, ... with 16-B loads, then the RG partial (max, first argmax) per channel
-// are merged through LDS (ties -> the smaller row, i.e. the first maximum like torch).
-__global__ __launch_bounds__(512) void audio_pool_norm_fwd_kernel(const bf16_t* __restrict__ a, float* __restrict__ an,
-                                                                  int* __restrict__ amax, float* __restrict__ anorm,
-                                                                  int HW, int C) {
-  __shared__ float sv[512 * 8];
-  __shared__ int si[512 * 8];
+// One block of 1024 threads per sample: thread = (8-channel block cg, row group rg); each thread
+// scans rows rg, rg + RG, ... with 16-B loads (four in flight), then the RG partial (max, first
+// argmax) per channel are merged through LDS (ties -> the smaller row, i.e. the first maximum like
+// torch).  Only B blocks: the per-thread row loop is the latency, so it is kept short.
+constexpr int kAPoolT = 1024;
+__device__ __forceinline__ void apool_take(const u32x4& v, int i, float* best, int* bi) {
+  const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float f = bf2f((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff));
+    if (f > best[e] || (f != f && best[e] == best[e])) {
+      best[e] = f;
+      bi[e] = i;
+    }
+  }
+}
+__global__ __launch_bounds__(kAPoolT) void audio_pool_norm_fwd_kernel(const bf16_t* __restrict__ a,
+                                                                      float* __restrict__ an, int* __restrict__ amax,
+                                                                      float* __restrict__ anorm, int HW, int C) {
+  __shared__ float sv[kAPoolT * 8];
+  __shared__ int si[kAPoolT * 8];
   __shared__ float red[16];
-  const int b = blockIdx.x, cvn = C / 8, RG = 512 / cvn;
+  const int b = blockIdx.x, cvn = C / 8, RG = kAPoolT / cvn;
   const int cg = threadIdx.x % cvn, rg = threadIdx.x / cvn;
   float best[8];
   int bi[8];
@@ -123,18 +136,15 @@ __global__ __launch_bounds__(512) void audio_pool_norm_fwd_kernel(const bf16_t* 
     bi[e] = 0;
   }
   const bf16_t* src = a + (size_t)b * HW * C + cg * 8;
-  for (int i = rg; i < HW; i += RG) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(src + (size_t)i * C);
-    const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+  int i = rg;
+  for (; i + 3 * RG < HW; i += 4 * RG) {  // rows taken in increasing order: the first max is kept
+    u32x4 v[4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float f = bf2f((e & 1) ? (u[e >> 1] >> 16) : (u[e >> 1] & 0xffff));
-      if (f > best[e] || (f != f && best[e] == best[e])) {
-        best[e] = f;
-        bi[e] = i;
-      }
-    }
+    for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const u32x4*>(src + (size_t)(i + k * RG) * C);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) apool_take(v[k], i + k * RG, best, bi);
   }
+  for (; i < HW; i += RG) apool_take(*reinterpret_cast<const u32x4*>(src + (size_t)i * C), i, best, bi);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     sv[rg * C + cg * 8 + e] = best[e];
@@ -246,7 +256,7 @@ extern "C" int avt_audio_pool_norm_fwd(const void* a, float* an, int* amax, floa
   AVT_REQUIRE(a && an && amax && anorm, "audio_pool_norm_fwd: null pointer");
   AVT_REQUIRE(C >= 64 && C <= 512 && (C & (C - 1)) == 0, "audio_pool_norm_fwd: C=%d unsupported", C);
   AVT_REQUIRE(HW > 0, "audio_pool_norm_fwd: empty map");
-  hipLaunchKernelGGL(audio_pool_norm_fwd_kernel, dim3(B), dim3(512), 0, (hipStream_t)stream, (const bf16_t*)a, an,
+  hipLaunchKernelGGL(audio_pool_norm_fwd_kernel, dim3(B), dim3(kAPoolT), 0, (hipStream_t)stream, (const bf16_t*)a, an,
                      amax, anorm, HW, C);
   return check_launch("audio_pool_norm_fwd");
 }
