@@ -263,23 +263,58 @@ __global__ __launch_bounds__(1024) void hardway_logits_kernel(const float* __res
 // one block of 1024 threads; wave w handles rows w, w+16, ... with lane-parallel max/sum
 __global__ __launch_bounds__(1024) void hardway_ce_kernel(const float* __restrict__ logits, int B, int L, float scale,
                                                           float* __restrict__ loss, float* __restrict__ dlogits) {
+  // one wave per row, the 16 waves' rows in groups of 4 whose loads are all issued up front (a row of
+  // L <= 256 logits is 4 values per lane); wider rows take the strided loop
   __shared__ float red[16];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int RG = 4;
   float part = 0.f;
-  for (int i = w; i < B; i += 16) {
-    const float* r = logits + (size_t)i * L;
-    float mx = -INFINITY;
-    for (int j = lane; j < L; j += 64) mx = fmaxf(mx, r[j]);
-    mx = wave_max(mx);
-    float se = 0.f;
-    for (int j = lane; j < L; j += 64) se += expf(r[j] - mx);
-    se = wave_sum(se);
-    const float lse = mx + logf(se);
-    if (lane == 0) part += lse - r[0];
-    if (dlogits) {
-      for (int j = lane; j < L; j += 64) {
-        const float sm = expf(r[j] - lse);
-        dlogits[(size_t)i * L + j] = (sm - (j == 0 ? 1.f : 0.f)) * scale / (float)B;
+  for (int i0 = w * RG; i0 < B; i0 += 16 * RG) {
+    if (L <= 256) {
+      float x[RG][4];
+#pragma unroll
+      for (int r = 0; r < RG; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int j = lane + 64 * k;
+          x[r][k] = (i0 + r < B && j < L) ? logits[(size_t)(i0 + r) * L + j] : -INFINITY;
+        }
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const int i = i0 + r;
+        if (i >= B) break;
+        const float mx = wave_max(fmaxf(fmaxf(x[r][0], x[r][1]), fmaxf(x[r][2], x[r][3])));
+        float se = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) se += lane + 64 * k < L ? expf(x[r][k] - mx) : 0.f;
+        se = wave_sum(se);
+        const float lse = mx + logf(se);
+        if (lane == 0) part += lse - x[r][0];
+        if (dlogits) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int j = lane + 64 * k;
+            if (j < L) dlogits[(size_t)i * L + j] = (expf(x[r][k] - lse) - (j == 0 ? 1.f : 0.f)) * scale / (float)B;
+          }
+        }
+      }
+      continue;
+    }
+    for (int i = i0; i < min(B, i0 + RG); ++i) {
+      const float* r = logits + (size_t)i * L;
+      float mx = -INFINITY;
+      for (int j = lane; j < L; j += 64) mx = fmaxf(mx, r[j]);
+      mx = wave_max(mx);
+      float se = 0.f;
+      for (int j = lane; j < L; j += 64) se += expf(r[j] - mx);
+      se = wave_sum(se);
+      const float lse = mx + logf(se);
+      if (lane == 0) part += lse - r[0];
+      if (dlogits) {
+        for (int j = lane; j < L; j += 64) {
+          const float sm = expf(r[j] - lse);
+          dlogits[(size_t)i * L + j] = (sm - (j == 0 ? 1.f : 0.f)) * scale / (float)B;
+        }
       }
     }
   }

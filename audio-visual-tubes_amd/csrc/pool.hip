@@ -205,10 +205,13 @@ __global__ void audio_pool_norm_bwd_kernel(const float* __restrict__ gan, const 
     am[c] = amax[(size_t)b * C + c];
   }
   __syncthreads();
-  // dense write of [HW][C] for sample b (8 channels per thread-iteration)
+  // dense write of rows [r0, r1) of the [HW][C] map of sample b (8 channels per thread-iteration);
+  // blockIdx.y slices the rows so that B x slices blocks share the store stream
   const int cv = C / 8;
+  const int rps = (HW + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rps, r1 = min(HW, r0 + rps);
   bf16_t* dst = ga + (size_t)b * HW * C;
-  for (int t = threadIdx.x; t < HW * cv; t += blockDim.x) {
+  for (int t = r0 * cv + threadIdx.x; t < r1 * cv; t += blockDim.x) {
     const int i = t / cv, c0 = (t - i * cv) * 8;
     float f[8];
 #pragma unroll
@@ -265,7 +268,8 @@ extern "C" int avt_audio_pool_norm_bwd(const float* gan, const float* an, const 
                                        int B, int HW, int C, void* stream) {
   AVT_REQUIRE(gan && an && amax && anorm && ga, "audio_pool_norm_bwd: null pointer");
   AVT_REQUIRE(C % 64 == 0 && C <= 1024, "audio_pool_norm_bwd: C=%d unsupported", C);
-  hipLaunchKernelGGL(audio_pool_norm_bwd_kernel, dim3(B), dim3(C), 0, (hipStream_t)stream, gan, an, amax, anorm,
+  AVT_REQUIRE(B > 0 && HW > 0, "audio_pool_norm_bwd: empty map");
+  hipLaunchKernelGGL(audio_pool_norm_bwd_kernel, dim3(B, min(HW, 8)), dim3(C), 0, (hipStream_t)stream, gan, an, amax, anorm,
                      (bf16_t*)ga, HW, C);
   return check_launch("audio_pool_norm_bwd");
 }
