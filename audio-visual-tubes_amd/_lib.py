@@ -65,6 +65,8 @@ SIGNATURES = {
     "avt_hardway_ce": (_I, [_P, _I, _I, _F, _P, _P, _P]),
     "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I,
                              _P]),
+    "avt_hardway_bwd_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                _P, _P, _I, _P]),
     "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "avt_localize_ciou": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
@@ -73,7 +75,7 @@ SIGNATURES = {
     "avt_spectrogram": (_I, [_P, _I, _L, _I, _F, _P, _P]),
     "avt_frames_transform": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
-    "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _P, _P, _P]),
+    "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _P, _P, _P, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_pack_desc_bytes": (_Z, []),
     "avt_pack_conv_weights_batched": (_I, [_P, _I, _L, _P]),
@@ -86,21 +88,52 @@ _lock = threading.Lock()
 _lib = None
 
 
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared"]
+HASH_PATH = LIB_PATH + ".sha256"
+
+
+def source_hash() -> str:
+    """sha256 over every csrc/*.hip, csrc/*.h, include/*.h and the compile flags: the identity of a
+    build.  build() records it next to libavt.so; lib() refuses a library whose record differs
+    (a stale .so shipped with newer sources)."""
+    import hashlib
+
+    h = hashlib.sha256(" ".join(HIPCC_FLAGS + SOURCES).encode())
+    inc = os.path.join(os.path.dirname(PKG_DIR), "include")
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    if os.path.isdir(inc):
+        files += sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h"))
+    for p in files:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _recorded_hash() -> str:
+    try:
+        with open(HASH_PATH) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
 def build(verbose: bool = False, force: bool = False) -> str:
-    """Compile csrc/*.hip for gfx950 into libavt.so (in-tree)."""
+    """Compile csrc/*.hip for gfx950 into libavt.so (in-tree); rebuilds whenever the sources' hash
+    differs from the one recorded at the last build."""
+    digest = source_hash()
+    if not force and os.path.exists(LIB_PATH) and _recorded_hash() == digest:
+        return LIB_PATH
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    if not force and os.path.exists(LIB_PATH):
-        deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-        newest = max(os.path.getmtime(s) for s in deps)
-        if os.path.getmtime(LIB_PATH) >= newest:
-            return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", tmp] + srcs
+    cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + srcs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(tmp, LIB_PATH)
+    with open(HASH_PATH, "w") as f:
+        f.write(digest + "\n")
     return LIB_PATH
 
 
@@ -112,6 +145,9 @@ def lib() -> ctypes.CDLL:
         if _lib is None:
             if not os.path.exists(LOAD_PATH):
                 raise RuntimeError(f"libavt.so not built ({LOAD_PATH}); run __graft_entry__.build()")
+            if LOAD_PATH == LIB_PATH and _recorded_hash() != source_hash():
+                raise RuntimeError(f"{LIB_PATH} was not built from the current csrc/ sources (hash record "
+                                   f"{HASH_PATH} differs); run __graft_entry__.build()")
             h = ctypes.CDLL(LOAD_PATH)
             for name, (res, args) in SIGNATURES.items():
                 if LOAD_PATH != LIB_PATH and not hasattr(h, name):

@@ -434,6 +434,32 @@ __global__ __launch_bounds__(256) void hardway_wa_bwd_kernel(const float* __rest
   }
 }
 
+// ---- gradients arriving through the returned A, Pos, Neg (model.py:124-135, returned at 154) ----
+// A[i,p] = A0[i,p,i]; Pos = sigmoid((A-eps1)/tau); Neg = 1 - sigmoid((A-eps2)/tau) (tri_map) or 1 - Pos:
+//   dA0[i,p,i] += gA + gPos * Pos(1-Pos)/tau - gNeg * Neg(1-Neg)/tau      (any of gA/gPos/gNeg may be NULL)
+// Runs after hardway_logits_bwd_kernel (read-modify-write of the diagonal it wrote).
+__global__ __launch_bounds__(256) void hardway_aux_bwd_kernel(const float* __restrict__ A0, const float* __restrict__ gA,
+                                                              const float* __restrict__ gPos,
+                                                              const float* __restrict__ gNeg, int B, int P, float eps1,
+                                                              float eps2, float tau, int trimap,
+                                                              float* __restrict__ dA0) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * P) return;
+  const int i = t / P, p = t - i * P;
+  const size_t d = ((size_t)i * P + p) * B + i;
+  const float x = A0[d], inv_t = 1.f / tau;
+  float g = gA ? gA[t] : 0.f;
+  if (gPos) {
+    const float w = sigm((x - eps1) * inv_t);
+    g += gPos[t] * w * (1.f - w) * inv_t;
+  }
+  if (gNeg) {
+    const float wn = trimap ? sigm(-(x - eps2) * inv_t) : sigm(-(x - eps1) * inv_t);
+    g -= gNeg[t] * wn * (1.f - wn) * inv_t;
+  }
+  dA0[d] += g;
+}
+
 // ---- the 16-frame two-view losses of train_hardway.py:134-142, one block of 1024 threads ----
 //   hardway = lw*CE1, aug = lw*CE2 (CE1/CE2: the hardway_ce outputs), l2 = (100-lw)*MSE(wA1, wA2),
 //   consistency = Prop(wA1) + Prop(wA2),  Prop(x) = mean |x[:,s+1] - x[:,s]| over (clip, s, p)
@@ -563,10 +589,13 @@ extern "C" int avt_hardway_ce(const float* logits, int B, int L, float scale, fl
 //   forward and the vision gradient (gv).
 //   outputs: gv [B][P][C] bf16 (grad of the vision layer4 map; dvh = gv = NULL skips it), gan [B][C] fp32
 //   (grad of the unit audio vectors; gan_accumulate = 1 adds to gan instead of overwriting it)
-extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
-                               const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
-                               int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh,
-                               void* gv, float* gan, int gan_accumulate, void* stream) {
+//   gA/gPos/gNeg [B][P] (each may be NULL): upstream gradients of the returned A, Pos, Neg maps
+//   (avt_hardway_bwd_ex; avt_hardway_bwd = all three NULL)
+extern "C" int avt_hardway_bwd_ex(const void* v, const float* an, const float* inv, const float* A0,
+                                  const float* save, const float* dlogits, int B, int P, int C, float eps1, float eps2,
+                                  float tau, int trimap, int use_neg, const float* dwA, const float* vsum, float* dm,
+                                  const float* gA, const float* gPos, const float* gNeg, float* dA0, float* dvh,
+                                  void* gv, float* gan, int gan_accumulate, void* stream) {
   AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && gan, "hardway_bwd: null pointer");
   AVT_REQUIRE((dvh == nullptr) == (gv == nullptr), "hardway_bwd: dvh and gv must be both set or both null");
   AVT_REQUIRE(dwA == nullptr || (vsum && dm && gv), "hardway_bwd: dwA needs vsum, dm and the vision gradient");
@@ -578,6 +607,9 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
                      tau, trimap, use_neg, dA0);
   if (dwA != nullptr)
     hipLaunchKernelGGL(hardway_wa_bwd_kernel, dim3(B), dim3(256), 0, st, A0, dwA, vsum, inv, B, P, C, eps1, tau, dA0, dm);
+  if (gA != nullptr || gPos != nullptr || gNeg != nullptr)
+    hipLaunchKernelGGL(hardway_aux_bwd_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, A0, gA, gPos, gNeg, B, P,
+                       eps1, eps2, tau, trimap, dA0);
   // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]   (skipped when the vision map is detached:
   // the tube head, whose video features come from a detached forward hook, model.py:12-15)
   if (gv != nullptr) sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
@@ -593,6 +625,14 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
     hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
                        dwA != nullptr ? dm : nullptr, (bf16_t*)gv, rows, C);
   return check_launch("hardway_bwd");
+}
+
+extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv, const float* A0, const float* save,
+                               const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
+                               int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh,
+                               void* gv, float* gan, int gan_accumulate, void* stream) {
+  return avt_hardway_bwd_ex(v, an, inv, A0, save, dlogits, B, P, C, eps1, eps2, tau, trimap, use_neg, dwA, vsum, dm,
+                            nullptr, nullptr, nullptr, dA0, dvh, gv, gan, gan_accumulate, stream);
 }
 
 // The 16-frame two-view loss combination (train_hardway.py:134-142) from the two CE values.

@@ -28,7 +28,8 @@ int check_launch(const char* what) {
   return AVT_OK;
 }
 
-// coef (optional): device {step_size, bc2_sqrt} written by adam_prep_kernel (graph-replayable form)
+// coef (optional): device {step_size, bc2_sqrt, beta1, beta2, eps, weight_decay} written by
+// adam_prep_kernel (graph-replayable form: the hyper-parameters are read on the device every launch)
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n,
                                                    float gscale, float b1, float b2, float eps, float wd,
@@ -36,6 +37,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   if (coef) {
     step_size = coef[0];
     bc2_sqrt = coef[1];
+    b1 = coef[2];
+    b2 = coef[3];
+    eps = coef[4];
+    wd = coef[5];
   }
   const long long nv = n / 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
@@ -233,14 +238,20 @@ __global__ void nhwc_to_nchw_kernel(const bf16_t* __restrict__ x, float* __restr
   }
 }
 
-// t = ++*step; coef = {lr / (1 - b1^t), sqrt(1 - b2^t)} in double, as the host path computes them
-__global__ void adam_prep_kernel(int* __restrict__ step, float lr, float b1, float b2, float* __restrict__ coef) {
+// t = ++*step; coef = {lr / (1 - b1^t), sqrt(1 - b2^t), b1, b2, eps, wd} in double, as the host
+// path computes them; hyper = device {lr, beta1, beta2, eps, weight_decay}
+__global__ void adam_prep_kernel(int* __restrict__ step, const float* __restrict__ hyper, float* __restrict__ coef) {
   const int t = *step + 1;
   *step = t;
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2];
   const double bc1 = 1.0 - pow((double)b1, t);
   const double bc2 = 1.0 - pow((double)b2, t);
   coef[0] = (float)(lr / bc1);
   coef[1] = (float)sqrt(bc2);
+  coef[2] = b1;
+  coef[3] = b2;
+  coef[4] = hyper[3];
+  coef[5] = hyper[4];
 }
 
 static int grid_for(long long n) {
@@ -277,20 +288,22 @@ extern "C" int avt_adam_step(float* param, const float* grad, float* exp_avg, fl
   return check_launch("adam_step");
 }
 
-// Same update with the step counter on the device (int, incremented here) and the bias
-// corrections computed there: every launch argument is step-invariant, so the call can be
-// captured once into a HIP graph and replayed.  coef: 2 floats of scratch.
+// Same update with the step counter AND the hyper-parameters on the device: hyper = {lr, beta1,
+// beta2, eps, weight_decay} (5 floats, read at every launch), step an int incremented here, the bias
+// corrections computed there.  Every launch argument is step-invariant, so the call can be captured
+// once into a HIP graph and replayed, and a learning-rate schedule (MultiStepLR,
+// train_hardway_1frame.py:118) or a restored checkpoint takes effect by writing `hyper`.
+// coef: AVT_ADAM_COEF_FLOATS floats of scratch.
 extern "C" int avt_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
-                                 float grad_scale, float lr, float beta1, float beta2, float eps, float weight_decay,
-                                 int* step, float* coef, void* stream) {
-  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq && step && coef, "adam_step_dev: null pointer");
+                                 float grad_scale, const float* hyper, int* step, float* coef, void* stream) {
+  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq && hyper && step && coef, "adam_step_dev: null pointer");
   AVT_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
               "adam_step_dev: buffers must be 16-byte aligned");
   if (n == 0) return AVT_OK;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step, lr, beta1, beta2, coef);
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step, hyper, coef);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, st, param, grad, exp_avg, exp_avg_sq, n,
-                     grad_scale, beta1, beta2, eps, weight_decay, 0.f, 0.f, (const float*)coef);
+                     grad_scale, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, (const float*)coef);
   return check_launch("adam_step_dev");
 }
 

@@ -272,7 +272,9 @@ class AVEngine:
         return y
 
     def forward(self, image: torch.Tensor, audio: torch.Tensor, training: bool, with_ce: bool = False,
-                ce_scale: float = 1.0):
+                ce_scale: float = 1.0, layer_io: bool = False):
+        """layer_io: also return each trunk's layer4 input/output ("v_in"/"v", "a_in"/"a", NHWC bf16)
+        for forward hooks registered on imgnet.layer4 / audnet.layer4 (test.py:63)."""
         if not image.is_cuda or not audio.is_cuda:
             raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
         if image.shape[1] != 3 or audio.shape[1] != 1:
@@ -287,9 +289,12 @@ class AVEngine:
             self._stat_arena.zero_()  # accumulators are re-zeroed by their finalize; this is belt and braces
         dev = image.device
 
+        io_a = {} if layer_io else None
+        io_v = {} if layer_io else None
+
         def audio_branch():
             xa = self._to_nhwc(audio, 1)
-            a, tape_a = self.aud.forward(xa, self.store, training)
+            a, tape_a = self.aud.forward(xa, self.store, training, io_a)
             C = a.shape[-1]
             an = torch.empty(B, C, device=dev, dtype=torch.float32)
             amax = torch.empty(B, C, device=dev, dtype=torch.int32)
@@ -302,7 +307,7 @@ class AVEngine:
             with self._branch():  # audio trunk (side stream) || vision trunk (current stream)
                 a, tape_a, an, amax, anorm = audio_branch()
         xi = self._to_nhwc(image, 4)
-        v, tape_i = self.img.forward(xi, self.store, training)
+        v, tape_i = self.img.forward(xi, self.store, training, io_v)
         if self.concurrent:
             self._join()
         else:
@@ -323,6 +328,8 @@ class AVEngine:
         call("avt_hardway_fwd", P(v), P(an), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map),
              int(self.neg), P(inv), P(vsum), P(A0), P(save), P(logits), P(A), P(Pos), P(Neg), P(wA), stream_ptr())
         out = {"A": A, "logits": logits, "weighted_A": wA, "Pos": Pos, "Neg": Neg, "v": v}
+        if layer_io:
+            out.update(v_in=io_v["layer4_in"], a=a, a_in=io_a["layer4_in"])
         tape = None
         if training:
             tape = {"img": tape_i, "aud": tape_a, "v": v, "a": a, "an": an, "amax": amax, "anorm": anorm,
@@ -360,9 +367,9 @@ class AVEngine:
         return [self.img, self.aud]
 
     def head_backward(self, tape, dlogits: Optional[torch.Tensor], dwA: Optional[torch.Tensor] = None,
-                      gan: Optional[torch.Tensor] = None):
-        """Hard-way head backward: (d logits, d weighted_A) -> (gv [B,h,w,C] bf16, gan [B,C] fp32).
-        A given ``gan`` is accumulated into (two views sharing one audio batch)."""
+                      gan: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None):
+        """Hard-way head backward: (d logits, d weighted_A[, d A, d Pos, d Neg]) -> (gv [B,h,w,C] bf16,
+        gan [B,C] fp32).  A given ``gan`` is accumulated into (two views sharing one audio batch)."""
         B, Pn, C = tape["B"], tape["P"], tape["C"]
         dev = tape["v"].device
         f32 = dict(device=dev, dtype=torch.float32)
@@ -378,19 +385,20 @@ class AVEngine:
         if dwA is not None:
             dwA = dwA.contiguous().float()
             dm = torch.empty(B, Pn, **f32)
-        call("avt_hardway_bwd", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
+        aux = [None if g is None else g.contiguous().float() for g in (dA, dPos, dNeg)]
+        call("avt_hardway_bwd_ex", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
              P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map), int(self.neg), P(dwA),
-             P(tape["vsum"] if dwA is not None else None), P(dm), P(dA0), P(dvh), P(gv), P(gan), int(accumulate),
-             stream_ptr())
+             P(tape["vsum"] if dwA is not None else None), P(dm), P(aux[0]), P(aux[1]), P(aux[2]), P(dA0), P(dvh),
+             P(gv), P(gan), int(accumulate), stream_ptr())
         return gv, gan
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
-                 dwA: Optional[torch.Tensor] = None):
+                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None):
         """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).  on_boundary(tag)
         is called as each grad_buckets() bucket becomes final (for an overlapped all-reduce).
         dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141)."""
         B, C = tape["B"], tape["C"]
-        gv, gan = self.head_backward(tape, dlogits, dwA)
+        gv, gan = self.head_backward(tape, dlogits, dwA, dA=dA, dPos=dPos, dNeg=dNeg)
         a = tape["a"]
         self.store.grads = self.flat.grad_views(gflat)
         par = on_boundary is None  # bucket hooks need the trunks in order on one stream
@@ -408,5 +416,48 @@ class AVEngine:
                 self.aud.backward(tape["aud"], ga, self.store, on_boundary)
                 on_boundary(self.aud.prefix + "lo")
             self._join(par)
+        finally:
+            self.store.grads = None
+
+
+class TrunkEngine(AVEngine):
+    """One ResNet-18 trunk called on its own (``model.imgnet(x)`` / a standalone ``resnet18(modal=...)``,
+    base_models.py:195-213): NCHW fp32 input -> layer4 map NCHW fp32, backward into the trunk's
+    parameter gradients (the stem's input gradient is not computed)."""
+
+    def __init__(self, flat: FlatStore, prefix: str, modal: str):
+        self._prefix, self._modal = prefix, modal
+        super().__init__(flat)
+        self.concurrent = False
+        self._nbt_idx = torch.tensor([i for i, n in enumerate(flat.nbt_names) if n.startswith(prefix)],
+                                     device=flat.flat.device, dtype=torch.long)
+
+    def _setup_trunks(self):
+        self.trunk = Trunk(self._prefix, self._modal)
+        self.trunks2d = [self.trunk]
+        self.bn_trunks = [self.trunk]
+
+    def forward(self, x: torch.Tensor, training: bool):
+        if not x.is_cuda:
+            raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
+        cin = 1 if self._modal == "audio" else 3
+        if x.dim() != 4 or x.shape[1] != cin:
+            raise ValueError(f"avt: {self._modal} trunk expects [N,{cin},H,W], got {tuple(x.shape)}")
+        self.pack_weights()
+        if training:
+            self.flat.nbt.index_add_(0, self._nbt_idx, torch.ones_like(self._nbt_idx))
+        xin = self._to_nhwc(x, self.trunk.stem.cp)
+        y, tape = self.trunk.forward(xin, self.store, training)
+        N, h, w, C = y.shape
+        out = torch.empty(N, C, h, w, device=x.device, dtype=torch.float32)
+        call("avt_nhwc_bf16_to_nchw", P(y), P(out), N, C, h * w, stream_ptr())
+        return out, tape
+
+    def backward(self, tape, g_out: torch.Tensor, gflat: torch.Tensor):
+        """g_out [N,512,h,w] fp32 (any layout) -> parameter gradients accumulated into gflat."""
+        g = g_out.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # layout plumbing
+        self.store.grads = self.flat.grad_views(gflat)
+        try:
+            self.trunk.backward(tape, g, self.store, None)
         finally:
             self.store.grads = None

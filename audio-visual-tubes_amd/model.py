@@ -9,6 +9,7 @@ Parameters.  Compute runs in libavt (HIP, gfx950); there is no CPU path.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -36,8 +37,10 @@ class BasicBlock(nn.Module):
 
 
 class ResNet(nn.Module):
-    """Parameter/buffer holder of base_models.ResNet(BasicBlock, [2,2,2,2], modal). Its compute
-    runs inside AVENet's engine; calling it alone is not supported."""
+    """base_models.ResNet(BasicBlock, [2,2,2,2], modal) on libavt.  Inside an AVENet its parameters are
+    views of the parent's flat storage; constructed on its own it keeps a flat store of its own.
+    ``forward(x)`` (base_models.py:195-213) returns the layer4 map [N,512,h,w] fp32 with gradients
+    into the parameters (not into x: the 7x7 stem's input gradient is not computed)."""
 
     def __init__(self, modal: str):
         super().__init__()
@@ -61,6 +64,12 @@ class ResNet(nn.Module):
             elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
+        self._avt_parent = None  # (weakref to the owning AVENet, prefix) once adopted
+        self._avt_engine = None
+        # a standalone trunk's flat storage is created at its first .to()/.cuda() (or forward): creating
+        # it here would turn the parameters into channels_last views before an enclosing AVENet re-inits
+        # them (model.py:104-110), and normal_ fills a channels_last view in another element order
+        self._own_flat = None
 
     def _make_layer(self, planes, blocks, stride):
         downsample = None
@@ -72,8 +81,88 @@ class ResNet(nn.Module):
             layers.append(BasicBlock(self.inplanes, planes))
         return nn.Sequential(*layers)
 
-    def forward(self, x):  # pragma: no cover - documented limitation
-        raise RuntimeError("avt: the trunks run inside AVENet.forward (fused engine); call the parent model")
+    def _trainable(self, name: str) -> bool:
+        """Parameters the standalone forward uses: the modal stem (base_models.py:197-200), bn1,
+        layer1-4; never conv1_flow, the other stem, fc."""
+        if name.startswith("fc.") or name == "conv1_flow.weight":
+            return False
+        return name != ("conv1.weight" if self.modal == "audio" else "conv1_a.weight")
+
+    def _adopt(self, parent, prefix: str):
+        """Called by the owning AVENet once its flat store holds this trunk's parameters."""
+        self._avt_parent = (weakref.ref(parent), prefix)
+        self._own_flat = None
+        self._avt_engine = None
+
+    def _flat_store(self) -> FlatStore:
+        if self._own_flat is None:
+            self._own_flat = FlatStore(self, lambda n, s=self: s._trainable(n))
+        return self._own_flat
+
+    def _apply(self, fn, recurse=True):
+        if self._avt_parent is not None and self._avt_parent[0]() is not None:
+            self._avt_parent[0]()._apply(fn)
+            return self
+        self._flat_store().apply(fn)
+        self._avt_engine = None
+        return self
+
+    def _engine_and_params(self):
+        from .engine import TrunkEngine
+
+        if self._avt_parent is not None:
+            parent, prefix = self._avt_parent[0](), self._avt_parent[1]
+            if parent is None:
+                raise RuntimeError("avt: the AVENet owning this trunk no longer exists")
+            flat = parent._flat
+        else:
+            parent, prefix, flat = self, "", self._flat_store()
+        if self._avt_engine is None or self._avt_engine.flat is not flat:
+            self._avt_engine = TrunkEngine(flat, prefix, self.modal)
+        named = dict(parent.named_parameters())
+        names = [n for n in flat.pnames if flat.trainable(n) and n.startswith(prefix)]
+        return self._avt_engine, flat, names, [named[n] for n in names]
+
+    def forward(self, x):
+        eng, flat, names, params = self._engine_and_params()
+        if x.requires_grad and torch.is_grad_enabled():
+            raise NotImplementedError("avt: gradients w.r.t. the trunk input are not computed (the reference "
+                                      "feeds data tensors; the 7x7 stem's dgrad is not built)")
+        need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in params)
+        if need_grad:
+            return _TrunkFunction.apply(eng, names, x, *params)
+        out, _ = eng.forward(x, self.training)
+        return out
+
+
+class _TrunkFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, names, x, *params):
+        out, tape = engine.forward(x, True)
+        ctx.engine, ctx.tape, ctx.names = engine, tape, names
+        ctx.set_materialize_grads(False)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return (None, None, None) + (None,) * len(ctx.names)
+        if ctx.tape is None:
+            raise RuntimeError("avt: second backward through a trunk forward")
+        flat = ctx.engine.flat
+        gflat = torch.zeros(flat.n_train, device=g.device, dtype=torch.float32)
+        ctx.engine.backward(ctx.tape, g, gflat)
+        ctx.tape = None
+        views = flat.param_grad_views(gflat)
+        return (None, None, None) + tuple(views[n] for n in ctx.names)
+
+
+class HardWayArgs:
+    """The argparse fields AVENet reads (model.py:98-102), with train_hardway_1frame.py:54-60's
+    defaults (--epsilon 0.65, --epsilon2 0.4, --tri_map / --Neg store_true default True)."""
+
+    def __init__(self, epsilon=0.65, epsilon2=0.4, tri_map=True, Neg=True):
+        self.epsilon, self.epsilon2, self.tri_map, self.Neg = epsilon, epsilon2, tri_map, Neg
 
 
 def resnet18(pretrained=False, progress=True, modal="vision", **kwargs):
@@ -86,10 +175,56 @@ def resnet18(pretrained=False, progress=True, modal="vision", **kwargs):
 # ---------------------------------------------------------------------------------------------
 
 
+def _nhwc_to_nchw_f32(x: torch.Tensor) -> torch.Tensor:
+    """NHWC bf16 trunk map -> NCHW fp32 (the reference layout/dtype of a ResNet layer output)."""
+    from ._lib import call
+    from .trunk import P, stream_ptr
+
+    N, H, W, C = x.shape
+    y = torch.empty(N, C, H, W, device=x.device, dtype=torch.float32)
+    call("avt_nhwc_bf16_to_nchw", P(x), P(y), N, C, H * W, stream_ptr())
+    return y
+
+
+# the only module hooks the fused engine can honour: forward hooks on each trunk's layer4 (test.py:63
+# registers one on imgnet.layer4 and reads its output for the layer-4 activation map, test.py:103)
+_HOOKABLE = ("imgnet.layer4", "audnet.layer4")
+
+
+def _check_hooks(model: nn.Module):
+    """Raise (before any state changes) on module hooks the fused engine cannot honour."""
+    for name, m in model.named_modules():
+        if not name.startswith(("imgnet", "audnet")):
+            continue
+        bad = bool(m._forward_pre_hooks) or bool(getattr(m, "_backward_hooks", None)) or bool(
+            getattr(m, "_backward_pre_hooks", None))
+        if m._forward_hooks and name not in _HOOKABLE:
+            bad = True
+        if bad:
+            raise NotImplementedError(
+                f"avt: hooks on `{name}` are not supported: the trunks run fused on the GPU; forward hooks "
+                f"are honoured on {', '.join(_HOOKABLE)} only")
+
+
+def _run_forward_hooks(module: nn.Module, inp: torch.Tensor, out: torch.Tensor):
+    """Call module's forward hooks as nn.Module.__call__ would: hook(module, (input,), output).  A hook
+    that returns a replacement output is not supported (the head already consumed the map)."""
+    for hid, hook in list(module._forward_hooks.items()):
+        if module._forward_hooks_with_kwargs.get(hid, False):
+            res = hook(module, (inp,), {}, out)
+        else:
+            res = hook(module, (inp,), out)
+        if res is not None:
+            raise NotImplementedError("avt: a forward hook on layer4 returned a replacement output; only "
+                                      "observing hooks (returning None) are supported")
+
+
 class _AVENetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine: AVEngine, training: bool, image, audio, *params):
-        out, tape = engine.forward(image, audio, training)
+    def forward(ctx, engine: AVEngine, training: bool, sink: Optional[dict], image, audio, *params):
+        out, tape = engine.forward(image, audio, training, layer_io=sink is not None)
+        if sink is not None:
+            sink.update(out)
         ctx.engine = engine
         ctx.tape = tape
         ctx.n_params = len(params)
@@ -98,27 +233,20 @@ class _AVENetFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gA, glogits, gwA, gPos, gNeg):
-        # the reference's train scripts back-propagate logits (CE, train_hardway_1frame.py:130-131) and
-        # weighted_A (MSE + PropagationLoss, train_hardway.py:138-141); A/Pos/Neg only feed eval/logging
-        for name, g in (("A", gA), ("Pos", gPos), ("Neg", gNeg)):
-            if g is not None and bool(torch.any(g != 0)):
-                raise NotImplementedError(
-                    f"avt: gradients through `{name}` are not implemented (no reference train script "
-                    "back-propagates it; see DESIGN.md)")
         engine: AVEngine = ctx.engine
         if ctx.tape is None:
             raise RuntimeError("avt: backward through an eval-mode forward (or a second backward)")
         nparams = ctx.n_params
-        if glogits is None and gwA is None:
-            return (None, None, None, None) + (None,) * nparams
+        if glogits is None and gwA is None and gA is None and gPos is None and gNeg is None:
+            return (None,) * 5 + (None,) * nparams
         flat = engine.flat
-        dev = (glogits if glogits is not None else gwA).device
+        dev = next(g for g in (glogits, gwA, gA, gPos, gNeg) if g is not None).device
         gflat = torch.zeros(flat.n_train, device=dev, dtype=torch.float32)
-        engine.backward(ctx.tape, glogits, gflat, dwA=gwA)
+        engine.backward(ctx.tape, glogits, gflat, dwA=gwA, dA=gA, dPos=gPos, dNeg=gNeg)
         ctx.tape = None
         views = flat.param_grad_views(gflat)
         grads = tuple(views.get(n) for n in flat.pnames[:nparams])
-        return (None, None, None, None) + grads
+        return (None,) * 5 + grads
 
 
 class AVENet(nn.Module):
@@ -143,11 +271,15 @@ class AVENet(nn.Module):
                 nn.init.constant_(m.bias, 0)
         self._flat = FlatStore(self)
         self._engine: Optional[AVEngine] = None
+        for prefix, net in (("imgnet.", self.imgnet), ("audnet.", self.audnet)):
+            net._adopt(self, prefix)
 
     # -- storage management: keep the flat buffers when moved (.cuda(), .to(dev)) --
     def _apply(self, fn, recurse=True):
         self._flat.apply(fn)
         self._engine = None
+        for net in (self.imgnet, self.audnet):
+            net._avt_engine = None
         return self
 
     def engine(self) -> AVEngine:
@@ -162,23 +294,26 @@ class AVENet(nn.Module):
         return [mods[n] for n in self._flat.pnames]
 
     def forward(self, image, audio):
+        _check_hooks(self)
+        hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
+                  if m._forward_hooks]
+        sink = {} if hooked else None
         eng = self.engine()
         params = self.ordered_parameters()
         n_train = sum(1 for n in self._flat.pnames if trainable(n))
         train_params = params[:n_train]
         need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in train_params)
         if need_grad:
-            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, image, audio, *train_params)
+            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, sink, image, audio, *train_params)
         else:
-            out, _ = eng.forward(image, audio, self.training)
+            out, _ = eng.forward(image, audio, self.training, layer_io=sink is not None)
             A, logits, wA, Pos, Neg = out["A"], out["logits"], out["weighted_A"], out["Pos"], out["Neg"]
-        hooks = self.imgnet.layer4._forward_hooks
-        if hooks:
-            self._run_layer4_hooks()
+            if sink is not None:
+                sink.update(out)
+        for name, m in hooked:  # test.py:63: activation['layer4'] = output.detach()
+            k_in, k_out = ("v_in", "v") if name == "imgnet" else ("a_in", "a")
+            _run_forward_hooks(m, _nhwc_to_nchw_f32(sink[k_in]), _nhwc_to_nchw_f32(sink[k_out]))
         return A, logits, wA, Pos, Neg
-
-    def _run_layer4_hooks(self):  # test.py:63 registers a forward hook on imgnet.layer4
-        raise NotImplementedError("avt: forward hooks on imgnet.layer4 are not supported yet")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -234,16 +369,16 @@ class _FullModelFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gA, glogits):
-        if gA is not None and bool(torch.any(gA != 0)):
-            raise NotImplementedError("avt: gradients through `A` are not implemented (train_3D.py back-propagates "
-                                      "the logits CE only)")
         nparams = ctx.n_params
-        if glogits is None:
+        if glogits is None and gA is None:
             return (None, None, None, None) + (None,) * nparams
         engine = ctx.engine
+        if ctx.tape is None:
+            raise RuntimeError("avt: backward through an eval-mode forward (or a second backward)")
         flat = engine.flat
-        gflat = torch.zeros(flat.n_train, device=glogits.device, dtype=torch.float32)
-        engine.backward(ctx.tape, glogits, gflat)
+        dev = (glogits if glogits is not None else gA).device
+        gflat = torch.zeros(flat.n_train, device=dev, dtype=torch.float32)
+        engine.backward(ctx.tape, glogits, gflat, dA=gA)
         ctx.tape = None
         views = flat.param_grad_views(gflat)
         return (None, None, None, None) + tuple(views.get(n) for n in flat.pnames[:nparams])
@@ -268,10 +403,12 @@ class FullModel(nn.Module):
 
         self._flat = FlatStore(self, tube_trainable)
         self._engine = None
+        self.audnet._adopt(self, "audnet.")
 
     def _apply(self, fn, recurse=True):
         self._flat.apply(fn)
         self._engine = None
+        self.audnet._avt_engine = None
         return self
 
     def engine(self):

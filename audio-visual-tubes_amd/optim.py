@@ -56,18 +56,66 @@ def _dense(t: torch.Tensor) -> bool:
 
 
 class FlatAdam:
-    """Adam state for the trainable region of a FlatStore.  The step count lives on the device
-    (``avt_adam_step_dev``), so a step is replayable from a captured HIP graph."""
+    """Adam state for the trainable region of a FlatStore.  The step count AND the hyper-parameters
+    live on the device (``avt_adam_step_dev`` reads them at every launch), so a step captured into
+    a HIP graph follows later changes: ``opt.lr = x`` / ``set_lr(x)`` (a MultiStepLR schedule,
+    train_hardway_1frame.py:118) or a restored checkpoint (checkpoint.load_flat_adam_state_dict)
+    takes effect in the next replay.  The setters are stream-ordered device writes (no host sync)."""
+
+    _HYPER = ("lr", "beta1", "beta2", "eps", "wd")
 
     def __init__(self, flat, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4):
         self.flat = flat
-        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         n = flat.n_train
         dev = flat.flat.device
         self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32)
         self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32)
         self.t_dev = torch.zeros(1, device=dev, dtype=torch.int32)
-        self._coef = torch.zeros(2, device=dev, dtype=torch.float32)
+        self._coef = torch.zeros(8, device=dev, dtype=torch.float32)  # AVT_ADAM_COEF_FLOATS
+        self._host = {"lr": float(lr), "beta1": float(betas[0]), "beta2": float(betas[1]), "eps": float(eps),
+                      "wd": float(weight_decay)}
+        self._hyper = torch.tensor([self._host[k] for k in self._HYPER], device=dev, dtype=torch.float32)
+
+    def _set(self, key: str, value: float):
+        self._host[key] = float(value)
+        # a (stream-ordered) H2D copy: every later launch, graph replays included, reads the new value
+        self._hyper[self._HYPER.index(key)] = float(value)
+
+    @property
+    def lr(self) -> float:
+        return self._host["lr"]
+
+    @lr.setter
+    def lr(self, v: float):
+        self._set("lr", v)
+
+    def set_lr(self, v: float):
+        self._set("lr", v)
+
+    @property
+    def betas(self):
+        return (self._host["beta1"], self._host["beta2"])
+
+    @betas.setter
+    def betas(self, v):
+        self._set("beta1", v[0])
+        self._set("beta2", v[1])
+
+    @property
+    def eps(self) -> float:
+        return self._host["eps"]
+
+    @eps.setter
+    def eps(self, v: float):
+        self._set("eps", v)
+
+    @property
+    def wd(self) -> float:
+        return self._host["wd"]
+
+    @wd.setter
+    def wd(self, v: float):
+        self._set("wd", v)
 
     @property
     def t(self) -> int:
@@ -76,5 +124,38 @@ class FlatAdam:
 
     def step(self, gflat: torch.Tensor, grad_scale: float = 1.0):
         call("avt_adam_step_dev", P(self.flat.flat), P(gflat), P(self.exp_avg), P(self.exp_avg_sq),
-             self.flat.n_train, grad_scale, self.lr, self.betas[0], self.betas[1], self.eps, self.wd, P(self.t_dev),
-             P(self._coef), stream_ptr())
+             self.flat.n_train, grad_scale, P(self._hyper), P(self.t_dev), P(self._coef), stream_ptr())
+
+
+class FlatMultiStepLR:
+    """torch.optim.lr_scheduler.MultiStepLR (train_hardway_1frame.py:118: milestones [60,100,150,180],
+    gamma 0.1, stepped once per epoch at :138) for a FlatAdam: lr = base_lr * gamma^(number of
+    milestones <= epoch).  Writes the device hyper-parameter, so captured step graphs follow."""
+
+    def __init__(self, opt: FlatAdam, milestones, gamma: float = 0.1, last_epoch: int = -1):
+        self.opt = opt
+        self.milestones = sorted(int(m) for m in milestones)
+        self.gamma = float(gamma)
+        self.base_lr = opt.lr
+        self.last_epoch = last_epoch
+        self.step()
+
+    def get_last_lr(self):
+        return [self.opt.lr]
+
+    def step(self):
+        self.last_epoch += 1
+        k = sum(1 for m in self.milestones if m <= self.last_epoch)
+        lr = self.base_lr * self.gamma ** k
+        if lr != self.opt.lr:
+            self.opt.set_lr(lr)
+
+    def state_dict(self):
+        return {"milestones": self.milestones, "gamma": self.gamma, "base_lr": self.base_lr,
+                "last_epoch": self.last_epoch}
+
+    def load_state_dict(self, sd):
+        self.milestones, self.gamma = list(sd["milestones"]), float(sd["gamma"])
+        self.base_lr, self.last_epoch = float(sd["base_lr"]), int(sd["last_epoch"])
+        k = sum(1 for m in self.milestones if m <= self.last_epoch)
+        self.opt.set_lr(self.base_lr * self.gamma ** k)

@@ -88,6 +88,9 @@ class HardWayTrainStep:
         """step(image, audio).  Returns the local mean CE loss (device scalar, no host sync)."""
         if self._graph is not None or self._seg_graphs is not None:
             return self._replay(*inputs)
+        return self._eager_step(*inputs)
+
+    def _eager_step(self, *inputs: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
             loss = self._fwd_bwd(*inputs)
             self.opt.step(self.grad, grad_scale=1.0)
@@ -172,6 +175,11 @@ class HardWayTrainStep:
         self._seg_graphs, self._seg_tags, self._graph_opt = graphs, tags, g_opt
 
     def _replay(self, *inputs: torch.Tensor) -> torch.Tensor:
+        if len(inputs) != len(self._static_in) or any(
+                tuple(x.shape) != tuple(s.shape) for s, x in zip(self._static_in, inputs)):
+            # e.g. the short last batch of a drop_last=False DataLoader: a copy_ would broadcast a
+            # 1-clip batch over all B rows (wrong negatives) -- run that batch eagerly instead
+            return self._eager_step(*inputs)
         for s, x in zip(self._static_in, inputs):
             if x is not s:
                 s.copy_(x)

@@ -207,8 +207,9 @@ class Trunk:
         stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, momentum=self.bn_momentum, rep=self.bn_rep)
         return y, stats, Pq, Qq
 
-    def forward(self, x: torch.Tensor, store: Store, training: bool):
-        """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape)."""
+    def forward(self, x: torch.Tensor, store: Store, training: bool, io: Optional[Dict] = None):
+        """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape).  io (optional) receives
+        "layer4_in": the layer3 output [N,h,w,256] (the input a forward hook on .layer4 sees)."""
         N, H, W, _ = x.shape
         tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
         c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
@@ -221,7 +222,9 @@ class Trunk:
              stream_ptr())
         tape.update(c0=c0, st0=st0, idx=idx, carg=carg, H1=H1, W1=W1)
         cur, Hc, Wc = p0, H2, W2
-        for blk in self.blocks:
+        for bi, blk in enumerate(self.blocks):
+            if io is not None and bi == 6:
+                io["layer4_in"] = cur
             t = {"x": cur, "H": Hc, "W": Wc}
             c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
             h1 = torch.empty_like(c1)

@@ -265,17 +265,19 @@ class TubeEngine(AVEngine):
     def backward_order(self):
         return [self.aud]
 
-    def backward(self, tape, dlogits: torch.Tensor, gflat: torch.Tensor, on_boundary=None):
-        """Accumulate d(loss)/d(audnet params) into gflat[:n_train] (caller zeroes it)."""
+    def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None, dA=None):
+        """Accumulate d(loss)/d(audnet params) into gflat[:n_train] (caller zeroes it).  dA (optional):
+        upstream gradient of the returned A map (model.py:60)."""
         B, Pn, C, rep, Ba = tape["B"], tape["P"], tape["C"], tape["rep"], tape["Ba"]
-        dev = dlogits.device
+        dev = tape["A0"].device
         f32 = dict(device=dev, dtype=torch.float32)
         dA0 = torch.empty(B, Pn, B, **f32)
         gan = torch.empty(B, C, **f32)
-        dlogits = dlogits.contiguous().float()
-        call("avt_hardway_bwd", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
-             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, None, None, None, P(dA0), None, None,
-             P(gan), 0, stream_ptr())
+        dlogits = torch.zeros(B, B + 2, **f32) if dlogits is None else dlogits.contiguous().float()
+        dA = None if dA is None else dA.contiguous().float()
+        call("avt_hardway_bwd_ex", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
+             P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, None, None, None, P(dA), None, None,
+             P(dA0), None, None, P(gan), 0, stream_ptr())
         if rep > 1:
             gan_a = torch.empty(Ba, C, **f32)
             call("avt_sum_rep_rows_f32", P(gan), P(gan_a), Ba, rep, C, stream_ptr())

@@ -86,8 +86,23 @@ def _cores():
     return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
 
 
-def _time_loop(fn, budget_s, max_n=50):
-    fn()  # warm-up
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def _time_loop(fn, budget_s, max_n=50, warmup=3):
+    """Median wall time of fn() after `warmup` untimed runs (>= 3 warm-ups, median)."""
+    for _ in range(warmup):
+        fn()
     times = []
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or len(times) < 3:
@@ -107,32 +122,42 @@ def cpu_baseline(workload: str, budget_s: float = 20.0):
 
     cores = _cores()
     torch.set_num_threads(cores)
+    cpu = _cpu_model()
     if workload == "twoview":
         t = 16
         sd = orc.make_state(0)
         fr, au, sp = orc.make_frames(1, t, 224, seed=3), orc.make_frames(1, t, 224, seed=4), orc.make_spectrogram(1)
         opt = orc.AdamRef(lr=4e-6)
-        med, n = _time_loop(lambda: orc.twoview_step(sd, fr, au, sp, opt), budget_s, max_n=10)
-        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port",
+        med, n = _time_loop(lambda: orc.twoview_step(sd, fr, au, sp, opt), budget_s, max_n=10, warmup=1)
+        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port", "cpu": cpu,
                 "sample": f"oracle fp32 train_hardway step (two views x 16 frames of 224^2, 16x-repeated 257x300 "
-                          f"spectrogram, both AVENet forwards + 3 losses + backward + Adam), b=1 clip, median of {n}"}
+                          f"spectrogram, both AVENet forwards + 3 losses + backward + Adam), b=1 clip, 1 warm-up, "
+                          f"median of {n}"}
     if workload == "tube":
         import tube_oracle as tor
 
         sd = tor.make_tube_state(0)
         video, spec = tor.make_video(1, 16, 224), orc.make_spectrogram(1)
         opt = orc.AdamRef()
-        med, n = _time_loop(lambda: tor.tube_train_step(sd, spec, video, opt), budget_s, max_n=10)
-        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port",
+        med, n = _time_loop(lambda: tor.tube_train_step(sd, spec, video, opt), budget_s, max_n=10, warmup=1)
+        return {"value": 1 / med, "unit": "clips/s", "cores": cores, "kind": "port", "cpu": cpu,
                 "sample": f"oracle fp32 train_3D step (R3D-18 fwd + 16x-repeated audio ResNet-18 fwd/bwd + head + "
-                          f"Adam), b=1 clip of 16x224^2 + 257x300, median of {n}"}
+                          f"Adam), b=1 clip of 16x224^2 + 257x300, 1 warm-up, median of {n}"}
     B = 2
     sd = orc.make_state(0)
     img, aud = orc.make_image(B), orc.make_spectrogram(B)
     opt = orc.AdamRef()
-    med, n = _time_loop(lambda: orc.train_step(sd, img, aud, opt), budget_s)
-    return {"value": B / med, "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"oracle fp32 full train step (fwd+CE+bwd+Adam), B=2, 224^2 + 257x300, median of {n}"}
+    med, n = _time_loop(lambda: orc.train_step(sd, img, aud, opt), budget_s * 0.6)
+
+    def fwd_loss():  # configs[0]: the reference's forward + loss on the CPU
+        with torch.no_grad():
+            orc.hardway_ce(orc.avenet_forward(sd, img, aud, None, training=True)[1])
+
+    med_f, n_f = _time_loop(fwd_loss, budget_s * 0.4)
+    return {"value": B / med, "unit": "clips/s", "cores": cores, "kind": "port", "cpu": cpu,
+            "fwd_loss_clips_per_s": B / med_f,
+            "sample": f"oracle fp32 full train step (fwd+CE+bwd+Adam), B=2, 224^2 + 257x300, 3 warm-ups, median of "
+                      f"{n}; fwd_loss_clips_per_s: forward + CE only (configs[0]), median of {n_f}"}
 
 
 def main():
@@ -158,25 +183,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:  # before any GPU call: a mismatch would report the wrong n_gpus
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 as "
+                 f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     import avtubes  # noqa: F401
-    from avt_amd.model import AVENet, FullModel
+    from avt_amd.model import AVENet, FullModel, HardWayArgs
     from avt_amd.train import HardWayTrainStep, TwoViewTrainStep
     from avt_amd.trunk import ConvProfiler
-
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import avenet_oracle as orc
 
     tube = args.workload == "tube"
     twoview = args.workload == "twoview"
     B = args.batch or (8 if (tube or twoview) else 128)
     torch.manual_seed(0)
     if twoview:
-        model = AVENet(orc.Args(), False).to(dev).train()
+        model = AVENet(HardWayArgs(), False).to(dev).train()
         frames, spec = synthetic_inputs(B, dev, seed=1000 + rank, frames=args.frames)
         augmented, _ = synthetic_inputs(B, dev, seed=2000 + rank, frames=args.frames)
         inputs = (frames, augmented, spec)
@@ -184,7 +209,7 @@ def main():
                     f"spectrogram ({'folded (b t) batch per view' if args.twoview_folded else 'audio once per clip'}),"
                     f" two AVENet forwards over (b t)={B * args.frames} rows, CE x2 + MSE + PropagationLoss, bwd, Adam")
     elif tube:
-        model = FullModel(orc.Args()).to(dev).train()
+        model = FullModel(HardWayArgs()).to(dev).train()
         video, spec = synthetic_inputs(B, dev, seed=1000 + rank, frames=args.frames)
         if args.tube_folded:  # train_3D.py:128-130
             spec = spec.unsqueeze(2).repeat(1, 1, args.frames, 1, 1).transpose(1, 2).reshape(
@@ -194,7 +219,7 @@ def main():
                     f"+ audio ResNet-18 fwd/bwd ({'folded (b t) batch' if args.tube_folded else 'once per clip'}) "
                     f"+ hard-way head over (b t)={B * args.frames} rows + CE + Adam")
     else:
-        model = AVENet(orc.Args(), False).to(dev).train()
+        model = AVENet(HardWayArgs(), False).to(dev).train()
         inputs = synthetic_inputs(B, dev, seed=1000 + rank)
         workload = "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam"
     if twoview:

@@ -176,6 +176,13 @@ int avt_hardway_bwd(const void* v, const float* an, const float* inv, const floa
                     const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
                     int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh, void* gv,
                     float* gan, int gan_accumulate, void* stream);
+/* avt_hardway_bwd plus the gradients arriving through the returned maps A, Pos, Neg (model.py:154;
+ * gA/gPos/gNeg [B][P] fp32, each may be NULL) */
+int avt_hardway_bwd_ex(const void* v, const float* an, const float* inv, const float* A0, const float* save,
+                       const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
+                       int use_neg, const float* dwA, const float* vsum, float* dm, const float* gA, const float* gPos,
+                       const float* gNeg, float* dA0, float* dvh, void* gv, float* gan, int gan_accumulate,
+                       void* stream);
 /* train_hardway.py:134-142 loss combination of the 16-frame two-view step: given the two CE values
  * (avt_hardway_ce outputs; their dlogits use scale loss_weight/2) and weighted_A of both views
  * ([b*t][P], '(b t)' clip-major), out[5] = {combined, hardway, aug, l2, consistency} and
@@ -212,11 +219,13 @@ int avt_frames_transform(const void* src, const long long* desc, int n, int S, i
 /* ---- optimizer / layout ---- */
 int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, float grad_scale,
                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, void* stream);
-/* avt_adam_step with the step count on the device (*step is incremented first) and the bias
- * corrections computed there into coef[2] — graph-capturable */
+/* avt_adam_step with the step count AND the hyper-parameters on the device: hyper = device float[5]
+ * {lr, beta1, beta2, eps, weight_decay}, read at every launch (a schedule or a restored checkpoint
+ * writes it; a captured graph follows); *step is incremented first and the bias corrections computed
+ * there into coef[AVT_ADAM_COEF_FLOATS] (scratch) — graph-capturable */
+#define AVT_ADAM_COEF_FLOATS 8
 int avt_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
-                      float grad_scale, float lr, float beta1, float beta2, float eps, float weight_decay, int* step,
-                      float* coef, void* stream);
+                      float grad_scale, const float* hyper, int* step, float* coef, void* stream);
 int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
                          void* stream);
 /* two launches (fwd copy, dgrad transpose) for many convs: descs = device array of n records

@@ -1,0 +1,262 @@
+"""Drop-in boundary behaviour beyond the train step's logits path:
+
+* forward hooks on ``imgnet.layer4`` (test.py:63 registers one and reads the activation, test.py:103);
+* gradients through the returned ``A``, ``Pos``, ``Neg`` maps (model.py:154);
+* calling a trunk on its own (``model.imgnet(x)``, a standalone ``resnet18(modal=...)``,
+  base_models.py:195-213) with gradients into its parameters;
+* a learning-rate change after ``HardWayTrainStep.capture()`` reaching the replayed Adam
+  (MultiStepLR, train_hardway_1frame.py:118);
+* a short last batch (DataLoader drop_last=False) after capture.
+
+Checkers: the fp64 oracle (oracle/avenet_oracle.py, pinned to the reference by the golden vectors).
+bf16-trunk tolerances as in test_model_gpu.py.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import avenet_oracle as orc
+from avt_amd._lib import call, query
+from avt_amd.model import AVENet, HardWayArgs, resnet18
+from avt_amd.optim import FlatMultiStepLR
+from avt_amd.train import HardWayTrainStep
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+_KEEP = []
+
+
+@pytest.fixture(autouse=True)
+def _keep_alive():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def P(t):
+    if t is None:
+        return None
+    _KEEP.append(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def S():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def cosine(a, b):
+    a, b = a.double().cpu().flatten(), b.double().cpu().flatten()
+    return float(a @ b / (a.norm() * b.norm()).clamp_min(1e-300))
+
+
+def _model(seed=0):
+    m = AVENet(HardWayArgs(), False)
+    m.load_state_dict(orc.make_state(seed))
+    return m.to(DEV).train()
+
+
+def _sd64(seed=0):
+    return {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in orc.make_state(seed).items()}
+
+
+# ------------------------------------------------------------------------------------------ head
+@pytest.mark.parametrize("B,trimap", [(6, True), (5, False)])
+def test_head_grads_through_A_Pos_Neg(B, trimap):
+    """avt_hardway_bwd_ex: d/d(v, an) of CE + <A,rA> + <Pos,rP> + <Neg,rN> vs fp64 autograd of the
+    oracle head (model.py:114-154) on the same bf16 features."""
+    C, h, w = 512, 14, 14
+    g = torch.Generator().manual_seed(31)
+    v = (torch.randn(B, h, w, C, generator=g).abs() + 0.3 * torch.rand(B, 1, 1, C, generator=g)).to(torch.bfloat16)
+    an = F.normalize(torch.randn(B, C, generator=g).abs() + 0.5, dim=1)
+    rA, rP, rN = (torch.randn(B, h * w, generator=g) for _ in range(3))
+    Pn, L = h * w, B + 2
+    f32 = dict(device=DEV, dtype=torch.float32)
+    vd, ad = v.to(DEV), an.to(DEV)
+    inv, vsum, A0 = torch.empty(B, Pn, **f32), torch.empty(B, Pn, **f32), torch.empty(B, Pn, B, **f32)
+    save = torch.empty(int(query("avt_hardway_save_floats", B)), **f32)
+    logits, A, Pos, Neg, wA = (torch.empty(B, L, **f32),) + tuple(torch.empty(B, Pn, **f32) for _ in range(4))
+    call("avt_hardway_fwd", P(vd), P(ad), B, Pn, C, 0.65, 0.4, 0.03, int(trimap), 1, P(inv), P(vsum), P(A0), P(save),
+         P(logits), P(A), P(Pos), P(Neg), P(wA), S())
+    loss, dl = torch.empty((), **f32), torch.empty(B, L, **f32)
+    call("avt_hardway_ce", P(logits), B, L, 1.0, P(loss), P(dl), S())
+    dA0, dvh, gv, gan = torch.empty(B, Pn, B, **f32), torch.empty(B, Pn, C, **f32), torch.empty_like(vd), \
+        torch.empty(B, C, **f32)
+    call("avt_hardway_bwd_ex", P(vd), P(ad), P(inv), P(A0), P(save), P(dl), B, Pn, C, 0.65, 0.4, 0.03, int(trimap), 1,
+         None, None, None, P(rA.to(DEV)), P(rP.to(DEV)), P(rN.to(DEV)), P(dA0), P(dvh), P(gv), P(gan), 0, S())
+    torch.cuda.synchronize()
+    vt = v.double().permute(0, 3, 1, 2).requires_grad_(True)
+    at = an.double().requires_grad_(True)
+    oA, olog, _, oPos, oNeg = orc.hardway_head(F.normalize(vt, dim=1), at, 0.65, 0.4, 0.03, trimap, True)
+    obj = (orc.hardway_ce(olog) + (oA.reshape(B, Pn) * rA.double()).sum() + (oPos.reshape(B, Pn) * rP.double()).sum()
+           + (oNeg.reshape(B, Pn) * rN.double()).sum())
+    obj.backward()
+    e_an, e_v = rel_err(gan, at.grad), rel_err(gv, vt.grad.permute(0, 2, 3, 1))
+    print(f"B={B} trimap={trimap}: rel err gan {e_an:.2e} gv {e_v:.2e}")
+    assert e_an < 2e-3 and e_v < 1e-2
+
+
+# ------------------------------------------------------------------------------------------ model
+def _tiny(b=4):
+    return orc.make_image(b, 64), orc.make_spectrogram(b, 65, 76)
+
+
+def test_layer4_forward_hook_matches_oracle():
+    """test.py:63,103: activation['layer4'] = output.detach(); torch.mean(activation, 1)."""
+    img, aud = _tiny()
+    model = _model().eval()
+    act = {}
+    calls = []
+
+    def hook(mod, inp, out):
+        calls.append(mod)
+        act["layer4"] = out.detach()
+        act["in"] = inp[0].detach()
+
+    h = model.imgnet.layer4.register_forward_hook(hook)
+    with torch.no_grad():
+        A, logits, _, _, _ = model(img.to(DEV), aud.to(DEV))
+    torch.cuda.synchronize()
+    assert calls == [model.imgnet.layer4]
+    sd = _sd64()
+    ref4 = orc.resnet18_forward(sd, "imgnet.", img.double(), "vision", training=False)
+    got = act["layer4"]
+    assert got.shape == ref4.shape and got.dtype == torch.float32
+    m_got, m_ref = torch.mean(got, 1).cpu().double(), torch.mean(ref4, 1)
+    err = ((m_got - m_ref).abs().max() / m_ref.abs().max()).item()
+    print(f"layer4 channel-mean rel err {err:.3e}; full map {rel_err(got, ref4):.3e}")
+    assert err < 3e-2 and rel_err(got, ref4) < 5e-2
+    assert act["in"].shape == (4, 256, 4, 4)
+    h.remove()
+    with torch.no_grad():
+        model(img.to(DEV), aud.to(DEV))
+    assert len(calls) == 1
+
+
+def test_unsupported_hook_raises_before_state_changes():
+    img, aud = _tiny()
+    model = _model()
+    model.imgnet.layer3.register_forward_hook(lambda *a: None)
+    before = model.state_dict()["imgnet.bn1.running_mean"].clone()
+    with pytest.raises(NotImplementedError):
+        model(img.to(DEV), aud.to(DEV))
+    assert torch.equal(before, model.state_dict()["imgnet.bn1.running_mean"])
+    assert int(model.state_dict()["imgnet.bn1.num_batches_tracked"]) == 0
+
+
+def test_grads_through_A_Pos_Neg_vs_oracle():
+    """A loss over all five outputs (model.py:154) back-propagates like the reference (fp64 oracle)."""
+    img, aud = _tiny()
+    B = img.shape[0]
+    g = torch.Generator().manual_seed(7)
+    rA, rP, rN = (0.05 * torch.randn(B, 1, 4, 4, generator=g) for _ in range(3))
+    model = _model()
+    A, logits, wA, Pos, Neg = model(img.to(DEV), aud.to(DEV))
+    assert A.shape == rA.shape
+    loss = (F.cross_entropy(logits, torch.zeros(B, dtype=torch.long, device=DEV)) + (A * rA.to(DEV)).sum()
+            + (Pos * rP.to(DEV)).sum() + (Neg * rN.to(DEV)).sum())
+    loss.backward()
+    sd = _sd64()
+    names = orc.trainable_names(sd)
+    leaves = {n: sd[n].clone().requires_grad_(True) for n in names}
+    work = dict(sd)
+    work.update(leaves)
+    oA, olog, _, oPos, oNeg = orc.avenet_forward(work, img.double(), aud.double(), None, training=True)
+    oloss = (orc.hardway_ce(olog) + (oA * rA.double()).sum() + (oPos * rP.double()).sum()
+             + (oNeg * rN.double()).sum())
+    grads = dict(zip(names, torch.autograd.grad(oloss, [leaves[n] for n in names])))
+    params = dict(model.named_parameters())
+    worst = 1.0
+    for n in ["imgnet.layer4.1.conv2.weight", "imgnet.layer3.0.conv1.weight", "audnet.layer4.1.conv2.weight",
+              "imgnet.layer4.1.bn2.weight", "audnet.layer2.0.conv1.weight"]:
+        c = cosine(params[n].grad, grads[n])
+        worst = min(worst, c)
+        print(f"{n}: cosine {c:.4f} norm ratio {params[n].grad.norm().item() / grads[n].norm().item():.4f}")
+    assert worst > 0.98
+
+
+def test_standalone_trunks_forward_backward():
+    """model.imgnet(x) and a standalone resnet18(modal='audio') (base_models.py:195-213): the layer4 map
+    and parameter gradients of <map, R> vs the fp64 oracle trunk."""
+    img, aud = _tiny()
+    model = _model()
+    sd = _sd64()
+    for net, x, prefix, modal in ((model.imgnet, img, "imgnet.", "vision"), (None, aud, "audnet.", "audio")):
+        if net is None:  # standalone, loaded from the audio trunk's weights
+            torch.manual_seed(0)
+            net = resnet18(modal="audio")
+            net.load_state_dict({k[len(prefix):]: v for k, v in orc.make_state(0).items() if k.startswith(prefix)})
+            net = net.to(DEV).train()
+            pfx = ""
+        else:
+            pfx = prefix
+        out = net(x.to(DEV))
+        ref_sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and ("weight" in k or "bias" in k)
+                      else v.clone()) for k, v in sd.items()}
+        ref = orc.resnet18_forward(ref_sd, prefix, x.double(), modal, training=True)
+        assert out.shape == ref.shape
+        e = rel_err(out, ref)
+        g = torch.Generator().manual_seed(3)
+        R = torch.randn(ref.shape, generator=g)
+        (out * R.to(DEV)).sum().backward()
+        (ref * R.double()).sum().backward()
+        params = dict(net.named_parameters())
+        for short in ["layer4.1.conv2.weight", "layer3.0.conv1.weight", "layer1.0.conv1.weight", "bn1.weight"]:
+            c = cosine(params[pfx + short].grad, ref_sd[prefix + short].grad)
+            print(f"{modal} {short}: cosine {c:.4f}")
+            assert c > 0.98, (modal, short, c)
+        print(f"{modal}: map rel err {e:.3e}")
+        assert e < 5e-2
+        # the unused stems / fc never get a gradient
+        assert params[pfx + ("conv1_flow.weight")].grad is None
+
+
+# ------------------------------------------------------------------------------------------ step
+def test_lr_change_after_capture_reaches_replays():
+    """Adam's hyper-parameters are read on the device by every replay (MultiStepLR)."""
+    img, aud = (t.to(DEV) for t in _tiny())
+    m_g, m_e = _model(), _model()
+    s_g = HardWayTrainStep(m_g, lr=1e-6, weight_decay=1e-4)
+    s_e = HardWayTrainStep(m_e, lr=1e-6, weight_decay=1e-4)
+    s_g.step(img, aud)
+    s_e.step(img, aud)
+    s_g.capture(img, aud)
+    sched = FlatMultiStepLR(s_g.opt, milestones=[1], gamma=0.0)  # lr -> 0 from "epoch" 1
+    sched.step()
+    assert s_g.opt.lr == 0.0
+    before = m_g._flat.flat.clone()
+    s_g.step(img, aud)  # replay with lr 0: weights (not BN buffers) unchanged
+    torch.cuda.synchronize()
+    assert torch.equal(before, m_g._flat.flat)
+    s_g.opt.lr = 3e-6  # replay with a new lr
+    s_e.opt.lr = 0.0
+    s_e.step(img, aud)
+    s_e.opt.lr = 3e-6
+    s_e.step(img, aud)
+    s_g.step(img, aud)
+    torch.cuda.synchronize()
+    assert s_g.opt.t == s_e.opt.t == 3
+    d = (m_g._flat.flat - before).abs().max().item()
+    assert 1e-6 < d <= 3e-6 * 1.05 + 1e-7, d
+    diff = (m_g._flat.flat - m_e._flat.flat).abs().max().item()
+    assert diff <= 1.1e-5, diff  # <= lr per step; split-K / BN atomics can flip a ~0 gradient's update
+
+
+def test_short_last_batch_after_capture_runs_eagerly():
+    img, aud = (t.to(DEV) for t in _tiny(4))
+    model = _model()
+    step = HardWayTrainStep(model, lr=1e-6, weight_decay=1e-4)
+    step.step(img, aud)
+    step.capture(img.clone(), aud.clone())
+    l_short = step.step(img[:1], aud[:1])  # one clip: CE over a [1, 3] logits row
+    l_full = step.step(img, aud)  # back to the replayed graph
+    torch.cuda.synchronize()
+    assert np.isfinite(l_short.item()) and np.isfinite(l_full.item())
+    assert step.opt.t == 3

@@ -106,3 +106,49 @@ def test_flat_adam_state_converts_to_and_from_torch_adam():
     topt2 = torch.optim.Adam(params, lr=1.0)
     topt2.load_state_dict(back)
     assert topt2.param_groups[0]["lr"] == 4e-6
+
+
+def _ref_cal_ciou(infer, gtmap, thres):
+    """utils.Evaluator.cal_CIOU (utils.py:209-214) transcribed line for line in numpy (the
+    reference's own arithmetic, independent of both the product and eval_oracle)."""
+    infer_map = np.zeros((224, 224))
+    infer_map[infer >= thres] = 1
+    ciou = np.sum(infer_map * gtmap) / (np.sum(gtmap) + np.sum(infer_map * (gtmap == 0)))
+    return ciou, np.sum(infer_map * gtmap), (np.sum(gtmap) + np.sum(infer_map * (gtmap == 0)))
+
+
+@pytest.mark.parametrize("n,seed", [(1, 60), (13, 61), (249, 62)])
+def test_auc_matches_sklearn_on_reference_grid(n, seed):
+    """utils.Evaluator.cal_AUC (utils.py:216-225) is sklearn.metrics.auc over x = [0.05 i, i=0..20]
+    of the fraction of maps with cIoU >= 0.05 i: the product and the restatement against sklearn
+    itself (importable here), incl. ties exactly on the grid and the 249-map test set size."""
+    from sklearn import metrics
+
+    rng = np.random.default_rng(seed)
+    cious = list(rng.random(n))
+    cious[: min(n, 3)] = [0.05 * k for k in (0, 10, 20)][: min(n, 3)]  # values on grid points
+    x = [0.05 * i for i in range(21)]
+    y = [np.sum(np.array(cious) >= 0.05 * i) / len(cious) for i in range(21)]
+    ref = metrics.auc(x, y)
+    e = ev.Evaluator()
+    e.ciou = list(cious)
+    assert abs(e.cal_AUC() - ref) < 1e-12, (e.cal_AUC(), ref)
+    assert abs(ev.auc_from_cious(cious) - ref) < 1e-12
+    assert abs(evo.cal_auc(cious) - ref) < 1e-12
+
+
+@pytest.mark.parametrize("thres", [0.5, 0.01, 0.0])
+def test_cal_ciou_matches_reference_transcription(thres):
+    """Evaluator.cal_CIOU on random maps (and the restatement) vs the line-for-line numpy transcription
+    of utils.py:209-214: identical (cIoU, intersection, denominator)."""
+    rng = np.random.default_rng(63)
+    for k in range(6):
+        infer = rng.random((224, 224)).astype(np.float32)
+        if k == 5:
+            infer[:] = thres  # every pixel exactly on the threshold
+        gt = (rng.random((224, 224)) < 0.3).astype(np.float64) * (0.5 if k % 2 else 1.0)
+        ref = _ref_cal_ciou(infer, gt, thres)
+        got = ev.Evaluator().cal_CIOU(infer, gt, thres)
+        assert got[1] == ref[1] and got[2] == ref[2] and abs(got[0] - ref[0]) < 1e-15, (got, ref)
+        rc = evo.cal_ciou(infer, gt, thres)
+        assert rc[1] == ref[1] and rc[2] == ref[2] and abs(rc[0] - ref[0]) < 1e-15

@@ -1,0 +1,189 @@
+"""Parity at BASELINE.json's full per-GPU configurations against golden vectors produced by the
+REFERENCE itself at those sizes (oracle/gen_golden_full.py: reference AVENet / FullModel in fp64):
+
+* configs[1] (the bench workload): B=128 clips of 224x224 RGB + 257x300 spectrogram;
+* configs[2]'s per-GPU shard: B=32 (256 clips over 8 GPUs, local negatives);
+* configs[3]'s per-GPU shard: FullModel, b=8 clips x 16 frames of 224x224 (b*t = 128 head rows).
+
+At these sizes BatchNorm reduces over up to 2.5 M rows per channel (the audio stem at B=128) through
+the fp64 slot accumulators, and the head contrasts 128 x 128 pairs.  Checked: loss, A, off-diagonal
+and diagonal logits, weighted_A, every per-parameter gradient norm, and the full running_mean /
+running_var of the largest-reduction BNs -- for the drop-in autograd path and for the fused
+HardWayTrainStep the bench times (eager, then replayed from its HIP graph).
+
+Tolerance = max(floor, 3 x the deviation of the REFERENCE's own trunks run under bf16 autocast with
+the fp32 head, measured at the same size by the generator) -- SURVEY §8(c)'s bf16 row, anchored as in
+test_model_gpu.py.  Running statistics: the implied batch mean within 2e-2 of the batch std and the
+implied unbiased batch variance within 2e-2 relative (bf16 conv operands, fp32/fp64 statistics).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import avenet_oracle as orc
+import tube_oracle as tor
+from gen_golden import checksum
+from avt_amd.model import AVENet, FullModel, HardWayArgs
+from avt_amd.train import HardWayTrainStep
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+FLOORS = {"A_abs": 1e-2, "logits_off_abs": 2e-2, "logits_diag_rel": 2e-3, "loss_rel": 1e-3, "wA_rel": 5e-2}
+
+
+def _golden(golden_dir, name):
+    path = os.path.join(golden_dir, name + ".npz")
+    if not os.path.exists(path):
+        pytest.skip(f"{name}.npz not generated")
+    return dict(np.load(path, allow_pickle=False))
+
+
+def _tol(g, k):
+    return max(FLOORS[k], 3 * float(g["bf16ref_dev/" + k]))
+
+
+def _check_outputs(g, A, logits, loss, wA=None, tag=""):
+    b = logits.shape[0]
+    off = ~np.eye(b, b + 2, k=1, dtype=bool)
+    diag = np.eye(b, b + 2, k=1, dtype=bool)
+    lg, l64 = logits.detach().cpu().double().numpy(), g["logits_f64"]
+    dev = {
+        "A_abs": np.abs(A.detach().cpu().double().numpy() - g["A_f64"]).max(),
+        "logits_off_abs": np.abs(lg[off] - l64[off]).max(),
+        "logits_diag_rel": (np.abs(lg[diag] - l64[diag]) / np.abs(l64[diag])).max(),
+        "loss_rel": abs(float(loss) - g["loss_f64"].item()) / abs(g["loss_f64"].item()),
+    }
+    if wA is not None:
+        w64 = g["weighted_A_f64"]
+        dev["wA_rel"] = np.abs(wA.detach().cpu().double().numpy() - w64).max() / np.abs(w64).max()
+    for k, v in dev.items():
+        tol = _tol(g, k)
+        print(f"{tag} {k} = {v:.3e} (bf16 reference {float(g['bf16ref_dev/' + k]):.3e}, tol {tol:.3e})")
+        assert v <= tol, (tag, k, v, tol)
+
+
+def _check_grad_norms(g, gn, tag=""):
+    rel = np.abs(gn - g["grad_norm_f64"]) / g["grad_norm_f64"]
+    dref = g["bf16ref_dev/gradnorm_rel"]
+    tol = np.maximum(np.maximum(5e-2, 3 * dref), 1.25 * dref.max())
+    names = [str(n) for n in g["param_names"]]
+    worst = names[int((rel / tol).argmax())]
+    print(f"{tag} grad-norm rel err max {rel.max():.3e} ({worst}) median {np.median(rel):.3e} "
+          f"(bf16 reference max {dref.max():.3e} median {np.median(dref):.3e})")
+    assert np.all(rel <= tol), (tag, worst, rel.max())
+    assert np.median(rel) <= 3 * np.median(dref) + 1e-3, (tag, np.median(rel))
+
+
+def _check_running_stats(g, sd, steps=1, tag=""):
+    """running = (1-0.1)^k * init + (1-0.9^k) * batch stat for k identical steps (init 0 / 1)."""
+    keys = sorted(k[len("buf_f64/"):-len(".running_mean")] for k in g if k.endswith(".running_mean"))
+    a1, ak = 0.1, 1 - 0.9 ** steps
+    for bn in keys:
+        rm64, rv64 = g[f"buf_f64/{bn}.running_mean"], g[f"buf_f64/{bn}.running_var"]
+        mean64, var64 = rm64 / a1, (rv64 - 0.9) / a1
+        rm, rv = sd[bn + ".running_mean"].cpu().double().numpy(), sd[bn + ".running_var"].cpu().double().numpy()
+        mean, var = rm / ak, (rv - 0.9 ** steps) / ak
+        em = np.abs(mean - mean64).max() / np.sqrt(var64.max())
+        ev = (np.abs(var - var64) / var64).max()
+        print(f"{tag} {bn}: batch-mean err {em:.2e} (of std), batch-var rel err {ev:.2e} over {len(rm)} channels")
+        assert em < 2e-2 and ev < 2e-2, (tag, bn, em, ev)
+
+
+def _avenet_inputs(g):
+    B = int(g["shape"][0])
+    img, aud = orc.make_image(B, 224), orc.make_spectrogram(B, 257, 300)
+    np.testing.assert_allclose(checksum(img), g["image_checksum"], rtol=1e-12)
+    np.testing.assert_allclose(checksum(aud), g["audio_checksum"], rtol=1e-12)
+    return img.to(DEV), aud.to(DEV)
+
+
+def _model():
+    m = AVENet(HardWayArgs(), False)
+    m.load_state_dict(orc.make_state(0))
+    return m.to(DEV).train()
+
+
+@pytest.mark.parametrize("name", ["avenet_cfg3_b32", "avenet_cfg2_b128"])
+def test_avenet_fullsize_autograd_vs_reference(golden_dir, name):
+    """The drop-in AVENet + nn.CrossEntropyLoss + autograd at the full per-GPU size."""
+    g = _golden(golden_dir, name)
+    img, aud = _avenet_inputs(g)
+    B = img.shape[0]
+    model = _model()
+    A, logits, wA, Pos, Neg = model(img, aud)
+    loss = F.cross_entropy(logits, torch.zeros(B, dtype=torch.long, device=DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    _check_outputs(g, A, logits, loss.item(), wA, tag=name)
+    params = dict(model.named_parameters())
+    names = [str(n) for n in g["param_names"]]
+    _check_grad_norms(g, np.array([params[n].grad.norm().item() for n in names]), tag=name)
+    _check_running_stats(g, model.state_dict(), 1, tag=name)
+    assert int(model.state_dict()["audnet.bn1.num_batches_tracked"]) == 1
+
+
+@pytest.mark.parametrize("name", ["avenet_cfg3_b32", "avenet_cfg2_b128"])
+def test_avenet_fullsize_fused_step_and_replay_vs_reference(golden_dir, name):
+    """The bench's HardWayTrainStep at the full size: the eager step, then the same step replayed from
+    its captured HIP graph (lr 0, so both see the initial weights; BN running stats compound)."""
+    g = _golden(golden_dir, name)
+    img, aud = _avenet_inputs(g)
+    model = _model()
+    step = HardWayTrainStep(model, lr=0.0, weight_decay=1e-4)
+    names = [str(n) for n in g["param_names"]]
+    for k, mode in enumerate(("eager", "graph replay")):
+        if k == 1:
+            step.capture(img, aud)
+        loss = step.step(img, aud)
+        torch.cuda.synchronize()
+        views = model._flat.grad_views(step.grad)
+        gn = np.array([views[n].norm().item() for n in names])
+        rel_loss = abs(loss.item() - g["loss_f64"].item()) / abs(g["loss_f64"].item())
+        print(f"{name} {mode}: loss {loss.item():.6f} (reference {g['loss_f64'].item():.6f}, rel {rel_loss:.2e})")
+        assert rel_loss <= _tol(g, "loss_rel")
+        _check_grad_norms(g, gn, tag=f"{name} {mode}")
+        _check_running_stats(g, model.state_dict(), k + 1, tag=f"{name} {mode}")
+    assert step.opt.t == 2
+
+
+def test_fullmodel_cfg4_vs_reference(golden_dir):
+    """configs[3] per GPU: FullModel over b=8 clips x 16 frames (R3D-18 layer4 detached, the
+    16-fold repeated spectrogram folded into (b t) = 128 rows), CE, backward; and the fused step with
+    the audio trunk run once per clip (exact de-dup, tube.py) on the same clips."""
+    g = _golden(golden_dir, "fullmodel_cfg4_b8t16")
+    b, t = int(g["shape"][0]), int(g["shape"][1])
+    video, spec = tor.make_video(b, t, 224), orc.make_spectrogram(b, 257, 300)
+    np.testing.assert_allclose(checksum(video), g["video_checksum"], rtol=1e-12)
+    np.testing.assert_allclose(checksum(spec), g["spec_checksum"], rtol=1e-12)
+    video, spec = video.to(DEV), spec.to(DEV)
+    folded = tor.repeat_spectrogram(spec, t)
+    names = [str(n) for n in g["param_names"]]
+
+    def fresh():
+        m = FullModel(HardWayArgs())
+        m.load_state_dict(tor.make_tube_state(0))
+        return m.to(DEV).train()
+
+    model = fresh()
+    A, logits = model(folded, video)
+    loss = F.cross_entropy(logits, torch.zeros(b * t, dtype=torch.long, device=DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    _check_outputs(g, A, logits, loss.item(), tag="cfg4 folded autograd")
+    params = dict(model.named_parameters())
+    _check_grad_norms(g, np.array([params[n].grad.norm().item() for n in names]), tag="cfg4 folded autograd")
+    _check_running_stats(g, model.state_dict(), 1, tag="cfg4 folded autograd")
+    # fused step, one spectrogram per clip (the bench's tube workload)
+    model2 = fresh()
+    step = HardWayTrainStep(model2, lr=0.0, weight_decay=1e-4)
+    loss2 = step.step(spec, video)
+    torch.cuda.synchronize()
+    rel = abs(loss2.item() - g["loss_f64"].item()) / abs(g["loss_f64"].item())
+    print(f"cfg4 fused de-dup: loss {loss2.item():.6f} rel {rel:.2e}")
+    assert rel <= _tol(g, "loss_rel")
+    views = model2._flat.grad_views(step.grad)
+    _check_grad_norms(g, np.array([views[n].norm().item() for n in names]), tag="cfg4 fused de-dup")
+    _check_running_stats(g, model2.state_dict(), 1, tag="cfg4 fused de-dup")

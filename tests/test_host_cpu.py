@@ -146,3 +146,27 @@ def test_fullmodel_refuses_cpu():
     m = FullModel(orc.Args())
     with pytest.raises(RuntimeError):
         m(orc.make_spectrogram(1, 65, 76), tor.make_video(1, 2, 32))
+
+
+def test_flat_multistep_lr_matches_torch_schedule():
+    """FlatMultiStepLR == torch.optim.lr_scheduler.MultiStepLR (train_hardway_1frame.py:118) epoch by
+    epoch, and every change lands in the device hyper-parameter vector the graph-replayable Adam reads."""
+    import types
+
+    from avt_amd.optim import FlatAdam, FlatMultiStepLR
+
+    flat = types.SimpleNamespace(n_train=8, flat=torch.zeros(8))
+    opt = FlatAdam(flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
+    sched = FlatMultiStepLR(opt, milestones=[60, 100, 150, 180], gamma=0.1)
+    p = torch.nn.Parameter(torch.zeros(1))
+    topt = torch.optim.Adam([p], lr=1e-3)
+    tsched = torch.optim.lr_scheduler.MultiStepLR(topt, milestones=[60, 100, 150, 180], gamma=0.1)
+    for epoch in range(200):
+        assert abs(opt.lr - topt.param_groups[0]["lr"]) <= 1e-12 * max(1.0, topt.param_groups[0]["lr"]), epoch
+        assert abs(float(opt._hyper[0]) - opt.lr) <= 1e-7 * opt.lr
+        topt.step()
+        tsched.step()
+        sched.step()
+    opt.betas = (0.8, 0.9)
+    opt.eps, opt.wd = 1e-6, 0.0
+    assert opt._hyper.tolist() == pytest.approx([opt.lr, 0.8, 0.9, 1e-6, 0.0])
