@@ -69,6 +69,8 @@ SIGNATURES = {
                                 _P, _P, _I, _P]),
     "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "avt_npratio_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "avt_flip_l1_loss": (_I, [_P, _P, _L, _I, _P, _P, _P, _P]),
     "avt_localize_ciou": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "avt_pair_ciou": (_I, [_P, _I, _I, _P, _P]),
     "avt_spectrogram_segments": (_I, [_L, _I]),

@@ -534,6 +534,61 @@ __global__ __launch_bounds__(1024) void propagation_loss_kernel(const float* __r
   if (threadIdx.x == 0) *loss = a * k;
 }
 
+// ---- NPRatio (losses.py:7-14) on x [b][t][P]: loss = mean_b mean_s |S[b,s+1] - S[b,s]|, S = sum_p x ----
+// one block; S kept in LDS (b*t <= kNpMaxRows); dx[b,s,p] = dloss/dS[b,s] for every p
+constexpr int kNpMaxRows = 4096;
+__global__ __launch_bounds__(1024) void npratio_loss_kernel(const float* __restrict__ x, int b, int t, int P,
+                                                            float* __restrict__ loss, float* __restrict__ dx) {
+  __shared__ float S[kNpMaxRows];
+  __shared__ float red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int rows = b * t;
+  for (int r = w; r < rows; r += nw) {
+    float a = 0.f;
+    for (int p = lane; p < P; p += 64) a += x[(size_t)r * P + p];
+    a = wave_sum(a);
+    if (lane == 0) S[r] = a;
+  }
+  __syncthreads();
+  const float k = 1.f / ((float)b * (float)(t - 1));
+  float acc = 0.f;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x)
+    if (r % t + 1 < t) acc += fabsf(S[r + 1] - S[r]);
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) *loss = acc * k;
+  if (dx) {
+    for (long long e = threadIdx.x; e < (long long)rows * P; e += blockDim.x) {
+      const int r = (int)(e / P), s = r % t;
+      float g = 0.f;
+      if (s + 1 < t) g -= sgnf(S[r + 1] - S[r]) * k;
+      if (s > 0) g += sgnf(S[r] - S[r - 1]) * k;
+      dx[e] = g;
+    }
+  }
+}
+
+// ---- FlipLoss (losses.py:25-36): nn.L1Loss()(y, hflip(x)) over rows of W (the last dim) ----
+// loss = mean |y[r,w] - x[r,W-1-w]|; dy = sgn(.)/n, dx[r,W-1-w] = -sgn(.)/n (sgn(0) = 0, as torch)
+__global__ __launch_bounds__(1024) void flip_l1_loss_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                            long long rows, int W, float* __restrict__ loss,
+                                                            float* __restrict__ dx, float* __restrict__ dy) {
+  __shared__ float red[16];
+  const long long n = rows * W;
+  const float inv_n = 1.f / (float)n;
+  float acc = 0.f;
+  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+    const long long r = e / W;
+    const int wc = (int)(e - r * W);
+    const long long ef = r * W + (W - 1 - wc);
+    const float d = y[e] - x[ef];
+    acc += fabsf(d);
+    if (dy) dy[e] = sgnf(d) * inv_n;
+    if (dx) dx[ef] = -sgnf(d) * inv_n;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) *loss = acc * inv_n;
+}
+
 __global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0.f;
@@ -651,4 +706,22 @@ extern "C" int avt_propagation_loss(const float* x, int b, int t, int P, float* 
   AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "propagation_loss: need b >= 1, t >= 2, P >= 1 (b=%d t=%d P=%d)", b, t, P);
   hipLaunchKernelGGL(propagation_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, b, t, P, loss, dx);
   return check_launch("propagation_loss");
+}
+
+// NPRatio (losses.py:7-14) of x [b][t][P]; dx (optional) = d(loss)/dx.
+extern "C" int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream) {
+  AVT_REQUIRE(x && loss, "npratio_loss: null pointer");
+  AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "npratio_loss: need b >= 1, t >= 2, P >= 1 (b=%d t=%d P=%d)", b, t, P);
+  AVT_REQUIRE((long long)b * t <= kNpMaxRows, "npratio_loss: b*t=%d exceeds %d", b * t, kNpMaxRows);
+  hipLaunchKernelGGL(npratio_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, b, t, P, loss, dx);
+  return check_launch("npratio_loss");
+}
+
+// FlipLoss (losses.py:25-36): L1(y, hflip(x)) over `rows` rows of W; dx / dy (optional) gradients.
+extern "C" int avt_flip_l1_loss(const float* x, const float* y, long long rows, int W, float* loss, float* dx,
+                                float* dy, void* stream) {
+  AVT_REQUIRE(x && y && loss, "flip_l1_loss: null pointer");
+  AVT_REQUIRE(rows >= 1 && W >= 1, "flip_l1_loss: empty input");
+  hipLaunchKernelGGL(flip_l1_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, y, rows, W, loss, dx, dy);
+  return check_launch("flip_l1_loss");
 }

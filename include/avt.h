@@ -31,6 +31,8 @@
  *   avt_twoview_loss             the 16-frame two-view loss of train_hardway.py:134-142: lw*CE x2, (100-lw)*
  *                                nn.MSELoss(weighted, weighted2), PropagationLoss x2 (losses.py:16-23)
  *   avt_propagation_loss         PropagationLoss.forward (losses.py:22-23) + its gradient
+ *   avt_npratio_loss             NPRatio.forward (losses.py:13-14) + its gradient (train_3D.py:113, 135)
+ *   avt_flip_l1_loss             FlipLoss.forward (losses.py:34-36) + its gradients
  *   avt_ncthw_to_nhwc_bf16       einops 'b c t h w -> (b t) c h w' of the frames (train_hardway.py:130-131)
  *   avt_localize_ciou,           the test loops' heatmap -> cIoU protocol (train_hardway_1frame.py:195-206,
  *   avt_pair_ciou                utils.Evaluator.cal_CIOU utils.py:209-214, utils.mTC 311-318)
@@ -191,6 +193,11 @@ int avt_twoview_loss(const float* ce1, const float* ce2, const float* wA1, const
                      float loss_weight, float* out, float* dwA1, float* dwA2, void* stream);
 /* PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (or NULL) = d(loss)/dx */
 int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
+/* NPRatio (losses.py:7-14) of x [b][t][P] (b*t <= 4096): mean |diff_t sum_p x|; dx (or NULL) = d(loss)/dx */
+int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
+/* FlipLoss (losses.py:25-36): nn.L1Loss()(y, hflip(x)) over `rows` rows of W; dx, dy (or NULL) gradients */
+int avt_flip_l1_loss(const float* x, const float* y, long long rows, int W, float* loss, float* dx, float* dy,
+                     void* stream);
 
 /* ---- localisation metrics (test loops of train_hardway*.py / test.py; utils.py:203-239, 311-318) ---- */
 /* A [N][h][w] heatmaps -> cv2 INTER_LINEAR resize to S x S, normalize_img(-.), 1 - ., median

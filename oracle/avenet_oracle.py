@@ -320,6 +320,18 @@ def propagation_loss(heatmap: torch.Tensor) -> torch.Tensor:
     return torch.abs(torch.diff(heatmap, dim=1)).mean(dim=(2, 3)).mean(dim=1).mean(dim=0)
 
 
+def npratio_loss(heatmap: torch.Tensor) -> torch.Tensor:
+    """NPRatio.forward (losses.py:13-14) on heatmap [b, t, h, w], restated from its text (losses.py is
+    not importable here: SURVEY §8c)."""
+    return torch.abs(torch.diff(torch.sum(heatmap, dim=(2, 3)), dim=1)).mean(dim=1).mean(dim=0)
+
+
+def flip_loss(heatmap: torch.Tensor, flipped_heatmap: torch.Tensor) -> torch.Tensor:
+    """FlipLoss.forward (losses.py:34-36): nn.L1Loss()(flipped_heatmap, RandomHorizontalFlip(p=1)(heatmap));
+    torchvision's tensor hflip is heatmap.flip(-1) (torchvision is absent here: restated)."""
+    return F.l1_loss(flipped_heatmap, heatmap.flip(-1))
+
+
 def twoview_losses(out1, out2, b: int, t: int, loss_weight: float = 0.1):
     """train_hardway.py:134-142 given the two AVENet outputs (A, logits, weighted_A, Pos, Neg).
     weighted.reshape(batch_size, frame_density, 14, 14) is written for the layer4 map's own (h, w).

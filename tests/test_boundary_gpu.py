@@ -151,8 +151,30 @@ def test_unsupported_hook_raises_before_state_changes():
     assert int(model.state_dict()["imgnet.bn1.num_batches_tracked"]) == 0
 
 
+def _oracle_aux_loss(sd, img, aud, rA, rP, rN, names, bf16=False):
+    """CE + <A,rA> + <Pos,rP> + <Neg,rN> through the oracle AVENet; bf16=True runs its trunks under CPU
+    bf16 autocast with the fp32 head (the yardstick configuration of oracle/gen_golden.py)."""
+    leaves = {n: sd[n].clone().requires_grad_(True) for n in names}
+    work = dict(sd)
+    work.update(leaves)
+    if bf16:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            v = orc.resnet18_forward(work, "imgnet.", img, "vision", True)
+            a = orc.resnet18_forward(work, "audnet.", aud, "audio", True)
+        v = F.normalize(v.float(), dim=1)
+        a = F.normalize(F.adaptive_max_pool2d(a.float(), 1).flatten(1), dim=1)
+        oA, olog, _, oPos, oNeg = orc.hardway_head(v, a)
+    else:
+        oA, olog, _, oPos, oNeg = orc.avenet_forward(work, img, aud, None, training=True)
+    dt = oA.dtype
+    oloss = (orc.hardway_ce(olog) + (oA * rA.to(dt)).sum() + (oPos * rP.to(dt)).sum() + (oNeg * rN.to(dt)).sum())
+    return dict(zip(names, torch.autograd.grad(oloss, [leaves[n] for n in names])))
+
+
 def test_grads_through_A_Pos_Neg_vs_oracle():
-    """A loss over all five outputs (model.py:154) back-propagates like the reference (fp64 oracle)."""
+    """A loss over all five outputs (model.py:154) back-propagates like the reference (fp64 oracle):
+    per-parameter gradient cosine and norm within the deviation of the reference's own trunks in
+    bf16 autocast on the same loss (tiny fixture: bf16 noise is large at 4x4 maps)."""
     img, aud = _tiny()
     B = img.shape[0]
     g = torch.Generator().manual_seed(7)
@@ -163,23 +185,18 @@ def test_grads_through_A_Pos_Neg_vs_oracle():
     loss = (F.cross_entropy(logits, torch.zeros(B, dtype=torch.long, device=DEV)) + (A * rA.to(DEV)).sum()
             + (Pos * rP.to(DEV)).sum() + (Neg * rN.to(DEV)).sum())
     loss.backward()
-    sd = _sd64()
-    names = orc.trainable_names(sd)
-    leaves = {n: sd[n].clone().requires_grad_(True) for n in names}
-    work = dict(sd)
-    work.update(leaves)
-    oA, olog, _, oPos, oNeg = orc.avenet_forward(work, img.double(), aud.double(), None, training=True)
-    oloss = (orc.hardway_ce(olog) + (oA * rA.double()).sum() + (oPos * rP.double()).sum()
-             + (oNeg * rN.double()).sum())
-    grads = dict(zip(names, torch.autograd.grad(oloss, [leaves[n] for n in names])))
+    names = orc.trainable_names(orc.make_state(0))
+    g64 = _oracle_aux_loss(_sd64(), img.double(), aud.double(), rA, rP, rN, names)
+    gbf = _oracle_aux_loss(orc.make_state(0), img, aud, rA, rP, rN, names, bf16=True)
     params = dict(model.named_parameters())
-    worst = 1.0
     for n in ["imgnet.layer4.1.conv2.weight", "imgnet.layer3.0.conv1.weight", "audnet.layer4.1.conv2.weight",
-              "imgnet.layer4.1.bn2.weight", "audnet.layer2.0.conv1.weight"]:
-        c = cosine(params[n].grad, grads[n])
-        worst = min(worst, c)
-        print(f"{n}: cosine {c:.4f} norm ratio {params[n].grad.norm().item() / grads[n].norm().item():.4f}")
-    assert worst > 0.98
+              "imgnet.layer4.1.bn2.weight", "audnet.layer2.0.conv1.weight", "imgnet.conv1.weight"]:
+        c, cr = cosine(params[n].grad, g64[n]), cosine(gbf[n], g64[n])
+        r = params[n].grad.norm().item() / g64[n].norm().item()
+        rr = gbf[n].norm().item() / g64[n].norm().item()
+        print(f"{n}: cosine {c:.4f} (bf16 reference {cr:.4f}), norm ratio {r:.4f} (bf16 reference {rr:.4f})")
+        assert c >= min(0.98, 1 - 3 * (1 - cr)), (n, c, cr)
+        assert abs(r - 1) <= max(5e-2, 3 * abs(rr - 1)), (n, r, rr)
 
 
 def test_standalone_trunks_forward_backward():
@@ -194,9 +211,6 @@ def test_standalone_trunks_forward_backward():
             net = resnet18(modal="audio")
             net.load_state_dict({k[len(prefix):]: v for k, v in orc.make_state(0).items() if k.startswith(prefix)})
             net = net.to(DEV).train()
-            pfx = ""
-        else:
-            pfx = prefix
         out = net(x.to(DEV))
         ref_sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and ("weight" in k or "bias" in k)
                       else v.clone()) for k, v in sd.items()}
@@ -209,13 +223,13 @@ def test_standalone_trunks_forward_backward():
         (ref * R.double()).sum().backward()
         params = dict(net.named_parameters())
         for short in ["layer4.1.conv2.weight", "layer3.0.conv1.weight", "layer1.0.conv1.weight", "bn1.weight"]:
-            c = cosine(params[pfx + short].grad, ref_sd[prefix + short].grad)
+            c = cosine(params[short].grad, ref_sd[prefix + short].grad)
             print(f"{modal} {short}: cosine {c:.4f}")
             assert c > 0.98, (modal, short, c)
         print(f"{modal}: map rel err {e:.3e}")
         assert e < 5e-2
         # the unused stems / fc never get a gradient
-        assert params[pfx + ("conv1_flow.weight")].grad is None
+        assert params["conv1_flow.weight"].grad is None and params["fc.weight"].grad is None
 
 
 # ------------------------------------------------------------------------------------------ step

@@ -150,6 +150,43 @@ def test_propagation_loss_module():
     assert rel_err(xd.grad, xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("b,t", [(3, 5), (8, 16), (1, 2)])
+def test_npratio_loss_module(b, t):
+    """losses.NPRatio (losses.py:7-14; train_3D.py:113, 135) vs its torch restatement in fp64."""
+    from avt_amd.losses import NPRatio
+
+    g = torch.Generator().manual_seed(34)
+    x = torch.rand(b, t, 14, 14, generator=g)
+    if t > 2:
+        x[:, 2] = x[:, 1]  # a tie: sgn(0) = 0
+    xd = x.to(DEV).requires_grad_(True)
+    loss = NPRatio()(xd)
+    loss.backward(torch.tensor(1.5, device=DEV))
+    xr = x.double().requires_grad_(True)
+    ref = orc.npratio_loss(xr)
+    (1.5 * ref).backward()
+    assert abs(loss.item() - ref.item()) < 2e-5 * max(1e-3, abs(ref.item()))
+    assert rel_err(xd.grad, xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [(4, 1, 14, 14), (2, 3, 7, 9), (5, 224)])
+def test_flip_loss_module(shape):
+    """losses.FlipLoss (losses.py:25-36): L1(flipped, hflip(heatmap)) and both gradients, fp64 ref."""
+    from avt_amd.losses import FlipLoss
+
+    g = torch.Generator().manual_seed(35)
+    x, y = torch.randn(*shape, generator=g), torch.randn(*shape, generator=g)
+    y.view(-1, shape[-1])[0] = x.view(-1, shape[-1])[0].flip(-1)  # exact zeros: sgn(0) = 0
+    xd, yd = x.to(DEV).requires_grad_(True), y.to(DEV).requires_grad_(True)
+    loss = FlipLoss()(xd, yd)
+    loss.backward(torch.tensor(0.7, device=DEV))
+    xr, yr = x.double().requires_grad_(True), y.double().requires_grad_(True)
+    ref = orc.flip_loss(xr, yr)
+    (0.7 * ref).backward()
+    assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
+    assert rel_err(xd.grad, xr.grad) < 1e-6 and rel_err(yd.grad, yr.grad) < 1e-6
+
+
 # ------------------------------------------------------------------------------ whole step
 FLOORS = {"logits_off_abs": 2e-2, "logits_diag_rel": 2e-3, "wA_rel": 5e-2}
 

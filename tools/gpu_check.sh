@@ -9,8 +9,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 rc=0
 if [ "$what" = all ] || [ "$what" = tests ]; then
-  timeout -k 10 600 python -m pytest tests -q -s -m gpu -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?
-  echo "tests rc=$rc"; tail -4 gpurun_out/gpu_tests.log
+  timeout -k 10 900 python -u -m pytest ${AVT_TESTS:-tests} -x -v -s -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?
+  echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" gpurun_out/gpu_tests.log | tail -8
   [ $rc -gt 1 ] && exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
   echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log
