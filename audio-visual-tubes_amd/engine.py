@@ -394,28 +394,40 @@ class AVEngine:
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
                  dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None):
-        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).  on_boundary(tag)
-        is called as each grad_buckets() bucket becomes final (for an overlapped all-reduce).
-        dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141)."""
-        B, C = tape["B"], tape["C"]
+        """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).
+        dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141); dA/dPos/dNeg:
+        of the returned maps.  The two trunks' backward runs concurrently (audio on the side stream) in
+        two segments: layer4+layer3 of both, then layer2..stem of both.  on_boundary(tags) is called
+        with ("imgnet.hi", "audnet.hi") between the segments and ("imgnet.lo", "audnet.lo") at the end
+        -- on the current stream, after the side stream has joined it, so a gradient all-reduce issued
+        there sees those buckets final (train.py overlaps them with the second segment)."""
         gv, gan = self.head_backward(tape, dlogits, dwA, dA=dA, dPos=dPos, dNeg=dNeg)
         a = tape["a"]
+        B, C = tape["B"], tape["C"]
         self.store.grads = self.flat.grad_views(gflat)
-        par = on_boundary is None  # bucket hooks need the trunks in order on one stream
+        hi = self.img.HI_BLOCK
+        seg = on_boundary is not None  # two segments (joined at the boundary) only when someone listens
         try:
-            with self._branch(par):  # audio backward (side stream) || vision backward
+            with self._branch():  # audio backward (side stream) || vision backward
                 ga = torch.empty_like(a)
                 call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
                      a.shape[1] * a.shape[2], C, stream_ptr())
-                if par:
-                    self.aud.backward(tape["aud"], ga, self.store, None)
-            self.img.backward(tape["img"], gv, self.store, on_boundary)
-            if on_boundary is not None:
-                on_boundary(self.img.prefix + "lo")
-            if not par:
-                self.aud.backward(tape["aud"], ga, self.store, on_boundary)
-                on_boundary(self.aud.prefix + "lo")
-            self._join(par)
+                ga = self.aud.backward_blocks(tape["aud"], ga, self.store, hi, len(self.aud.blocks))
+                if not seg:
+                    ga = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi)
+                    self.aud.backward_stem(tape["aud"], ga, self.store)
+            gv = self.img.backward_blocks(tape["img"], gv, self.store, hi, len(self.img.blocks))
+            if seg:
+                self._join()
+                on_boundary((self.img.prefix + "hi", self.aud.prefix + "hi"))
+                with self._branch():  # second segment
+                    ga = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi)
+                    self.aud.backward_stem(tape["aud"], ga, self.store)
+            gv = self.img.backward_blocks(tape["img"], gv, self.store, 0, hi)
+            self.img.backward_stem(tape["img"], gv, self.store)
+            self._join()
+            if seg:
+                on_boundary((self.img.prefix + "lo", self.aud.prefix + "lo"))
         finally:
             self.store.grads = None
 

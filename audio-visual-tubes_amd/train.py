@@ -9,13 +9,15 @@ semantics); gradients are summed with ONE all-reduce of the flat fp32 gradient b
 (backend "nccl"), the 1/world factor is folded into the Adam kernel, and BN running statistics
 follow rank 0 (DDP ``broadcast_buffers``, matching DP's replica-0 buffers).
 
-The all-reduce is bucketed and overlapped with backward: the flat gradient splits into one bucket
-per trunk for layer3+layer4 (~42 MB, 94 % of a ResNet-18's parameters) and one for the rest; each
-bucket's RCCL all-reduce is launched (async, on RCCL's stream) the moment the backward has
-finished it, so the vision trunk's buckets travel while the audio trunk's backward runs and the
-audio layer3/4 bucket while its layer2..stem run.  Only the last ~2.7 MB bucket is exposed.  With a
-captured step the backward is recorded as one HIP graph per bucket boundary (sharing one memory
-pool, replayed in capture order) and the collectives are issued between the replays.
+The all-reduce is bucketed and overlapped with backward, with the two trunks still running
+concurrently: the flat gradient splits into one bucket per trunk for layer3+layer4 (~42 MB each, 94 %
+of a ResNet-18's parameters) and one for the rest (~2.7 MB).  The backward runs as two segments --
+layer4+layer3 of both trunks (audio on a second HIP stream), then layer2..stem of both -- and the two
+"hi" buckets' RCCL all-reduces are launched (async, on RCCL's stream) at the boundary, so they travel
+over xGMI while the second segment computes; only the two small "lo" buckets are exposed.  With a
+captured step each segment is one HIP graph (sharing one memory pool, replayed in capture order) and
+the collectives are issued between the replays.  (TwoView/Tube engines call the boundary once per
+trunk, sequentially.)
 """
 from __future__ import annotations
 
@@ -49,7 +51,7 @@ def sync_buffers(bflat: torch.Tensor, pg: Optional[dist.ProcessGroup] = None):
 
 class HardWayTrainStep:
     def __init__(self, model, lr: float = 1e-6, weight_decay: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 process_group: Optional[dist.ProcessGroup] = None, engine=None, overlap_allreduce: bool = False):
+                 process_group: Optional[dist.ProcessGroup] = None, engine=None, overlap_allreduce: bool = True):
         self.model = model
         self.engine: AVEngine = engine if engine is not None else model.engine()
         self.flat = model._flat
@@ -57,13 +59,9 @@ class HardWayTrainStep:
         self.grad = torch.zeros(self.flat.n_train, device=self.flat.flat.device, dtype=torch.float32)
         self.pg = process_group
         self.world = world_size(process_group)
-        # world > 1: either ONE all-reduce of the flat gradient after a backward that runs the two
-        # trunks concurrently (default), or per-bucket all-reduces overlapped with a sequential
-        # backward (overlap_allreduce).  Measured on one MI355X the trunk concurrency is worth ~12 %
-        # of the step; the 89 MB all-reduce over xGMI ~0.5 ms (~4 %), so concurrency wins.
+        # world > 1: per-bucket all-reduces overlapped with the second backward segment (default), or
+        # ONE all-reduce of the whole flat gradient after the backward (overlap_allreduce=False)
         self.overlap = overlap_allreduce and self.world > 1
-        if self.overlap:
-            self.engine.concurrent = False  # the bucket hooks follow the trunks on one stream
         if self.world > 1:
             # start from identical weights everywhere (DDP constructor semantics)
             dist.broadcast(self.flat.flat, 0, group=self.pg)
@@ -80,9 +78,12 @@ class HardWayTrainStep:
         self.engine.backward(tape, out["dlogits"], self.grad, on_boundary)
         return out["loss"]
 
-    def _allreduce_bucket(self, tag: str, works: list):
-        lo, hi = self.buckets[tag]
-        works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+    def _allreduce_bucket(self, tags, works: list):
+        """Issue the async all-reduce of the bucket(s) a backward boundary made final (one tag, or a
+        tuple of tags reached together); RCCL's stream waits for the current stream's work so far."""
+        for tag in ((tags,) if isinstance(tags, str) else tags):
+            lo, hi = self.buckets[tag]
+            works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
     def step(self, *inputs: torch.Tensor) -> torch.Tensor:
         """step(image, audio).  Returns the local mean CE loss (device scalar, no host sync)."""
@@ -102,7 +103,7 @@ class HardWayTrainStep:
             self.opt.step(self.grad, grad_scale=1.0 / self.world)
             return loss
         works: list = []
-        loss = self._fwd_bwd(*inputs, on_boundary=lambda tag: self._allreduce_bucket(tag, works))
+        loss = self._fwd_bwd(*inputs, on_boundary=lambda tags: self._allreduce_bucket(tags, works))
         for w in works:  # the current stream waits for RCCL's (no host sync)
             w.wait()
         self.opt.step(self.grad, grad_scale=1.0 / self.world)
@@ -157,13 +158,14 @@ class HardWayTrainStep:
             def boundary(tag):
                 graphs[-1].capture_end()
                 tags.append(tag)
-                if tag != last_tag:  # nothing is launched after the last bucket's boundary
+                got = (tag,) if isinstance(tag, str) else tuple(tag)
+                if last_tag not in got:  # nothing is launched after the last bucket's boundary
                     g2 = torch.cuda.CUDAGraph()
                     g2.capture_begin(pool=pool)
                     graphs.append(g2)
 
             loss = self._fwd_bwd(*inputs, on_boundary=boundary)
-            if not tags or tags[-1] != last_tag:
+            if not tags or last_tag not in ((tags[-1],) if isinstance(tags[-1], str) else tuple(tags[-1])):
                 raise RuntimeError("avt: backward did not reach its last gradient bucket")
             g_opt = torch.cuda.CUDAGraph()
             g_opt.capture_begin(pool=pool)

@@ -295,11 +295,18 @@ class Trunk:
     HI_BLOCK = 4  # index of layer3.0 in self.blocks
 
     def backward(self, tape: Dict, g_out: torch.Tensor, store: Store, on_boundary=None):
+        g = self.backward_blocks(tape, g_out, store, self.HI_BLOCK, len(self.blocks))
+        if on_boundary is not None:
+            on_boundary(self.prefix + "hi")
+        g = self.backward_blocks(tape, g, store, 0, self.HI_BLOCK)
+        self.backward_stem(tape, g, store)
+
+    def backward_blocks(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int) -> torch.Tensor:
+        """Backward of blocks hi-1 .. lo (BasicBlock.forward, base_models.py:53-69); returns the gradient
+        of block lo's input."""
         N = tape["N"]
-        g = g_out
-        for bi, blk, t in zip(reversed(range(len(self.blocks))), reversed(self.blocks), reversed(tape["blocks"])):
-            if on_boundary is not None and bi == self.HI_BLOCK - 1:
-                on_boundary(self.prefix + "hi")
+        for bi in reversed(range(lo, hi)):
+            blk, t = self.blocks[bi], tape["blocks"][bi]
             Hc, Wc, Ho, Wo = t["H"], t["W"], t["Ho"], t["Wo"]
             identity = blk["down"] is None
             gsum = torch.empty_like(t["c2"]) if identity else None
@@ -316,7 +323,11 @@ class Trunk:
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store)
                 g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True)
             g = g_x
-        # maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)
+        return g
+
+    def backward_stem(self, tape: Dict, g: torch.Tensor, store: Store):
+        """maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)."""
+        N = tape["N"]
         H1, W1 = tape["H1"], tape["W1"]
         c0, st0 = tape["c0"], tape["st0"]
         g_c0 = torch.empty_like(c0)

@@ -41,6 +41,40 @@ def _peak_gb():
     return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2 ** 20
 
 
+def avenet_bf16_trunks(ref_model, sd, image, audio):
+    """gen_golden.run_reference_bf16_trunks, also returning the BN buffers the bf16 forward updated."""
+    import torch.nn.functional as F
+
+    net = ref_model.AVENet(orc.Args(), False)
+    net.load_state_dict(sd, strict=True)
+    net.train()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        img = net.imgnet(image)
+        aud = net.audnet(audio)
+    img = F.normalize(img.float(), dim=1)
+    aud = F.normalize(F.adaptive_max_pool2d(aud.float(), 1).flatten(1), dim=1)
+    A, logits, wA, Pos, Neg = orc.hardway_head(img, aud)
+    loss = torch.nn.CrossEntropyLoss()(logits, torch.zeros(logits.shape[0], dtype=torch.long))
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+    bufs = {n: b.detach().clone() for n, b in net.named_buffers()}
+    return dict(A=A.detach(), logits=logits.detach(), weighted_A=wA.detach(), loss=loss.detach(), grads=grads,
+                bufs=bufs)
+
+
+def bn_stat_dev(bufs, bufs64, bns):
+    """Per BN: max |batch mean - fp64| / max fp64 batch std, and max relative error of the unbiased
+    batch variance, both recovered from one momentum-0.1 update of (0, 1) running stats."""
+    out = {}
+    for bn in bns:
+        m64 = bufs64[bn + ".running_mean"].double().numpy() / 0.1
+        v64 = (bufs64[bn + ".running_var"].double().numpy() - 0.9) / 0.1
+        m = bufs[bn + ".running_mean"].double().numpy() / 0.1
+        v = (bufs[bn + ".running_var"].double().numpy() - 0.9) / 0.1
+        out[bn] = (np.abs(m - m64).max() / np.sqrt(v64.max()), (np.abs(v - v64) / v64).max())
+    return out
+
+
 def avenet_fixture(ref_model, name, batch, seed_w=0):
     sd = orc.make_state(seed_w, torch.float32)
     image = orc.make_image(batch, 224)
@@ -70,9 +104,7 @@ def avenet_fixture(ref_model, name, batch, seed_w=0):
     del net, A, logits, wA, Pos, Neg, loss, grads
     # yardstick: the reference's trunks under bf16 autocast, fp32 head (gen_golden.run_reference_bf16_trunks)
     t0 = time.time()
-    from gen_golden import run_reference_bf16_trunks
-
-    rb = run_reference_bf16_trunks(ref_model, sd, image, audio)
+    rb = avenet_bf16_trunks(ref_model, sd, image, audio)
     print(f"[{name}] bf16-trunk reference {time.time() - t0:.0f} s", flush=True)
     off = ~np.eye(batch, batch + 2, k=1, dtype=bool)
     diag = np.eye(batch, batch + 2, k=1, dtype=bool)
@@ -88,6 +120,9 @@ def avenet_fixture(ref_model, name, batch, seed_w=0):
     }
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
+    for bn, (em, ev) in bn_stat_dev(rb["bufs"], bufs, FULL_BUFS).items():
+        out["bf16ref_dev/bnstat/" + bn] = np.array([em, ev])
+        print(f"[{name}] bf16-trunk reference {bn}: batch-mean err {em:.2e} of std, batch-var rel err {ev:.2e}")
     print(f"[{name}] bf16-trunk reference deviation: " + ", ".join(
         f"{k}={np.max(v):.3e}" + (f" (median {np.median(v):.3e})" if np.ndim(v) else "") for k, v in dev.items()))
     out["image_checksum"] = checksum(image)
@@ -97,8 +132,29 @@ def avenet_fixture(ref_model, name, batch, seed_w=0):
     print(f"[{name}] loss f64 {out['loss_f64'].item():.9f} -> {path}", flush=True)
 
 
+def tube_bf16(ref_model, sd, spec, video):
+    """gen_golden_tube.run_reference_bf16_trunks, also returning the BN buffers."""
+    import torch.nn.functional as F
+
+    net = ref_model.FullModel(orc.Args())
+    net.load_state_dict(sd, strict=True)
+    net.train()
+    audio = tor.repeat_spectrogram(spec, video.shape[2])
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        aud = net.audnet(audio)
+        with torch.no_grad():  # the hook detaches layer4 (model.py:15): no vidnet gradient either way
+            net.vidnet(video)
+    vid = F.normalize(ref_model.activation["layer4"].float(), dim=1)
+    aud = F.normalize(F.adaptive_max_pool2d(aud.float(), 1).flatten(1), dim=1)
+    A, logits = orc.hardway_attention(aud, vid)
+    loss = torch.nn.CrossEntropyLoss()(logits, torch.zeros(logits.shape[0], dtype=torch.long))
+    loss.backward()
+    grads = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+    bufs = {n: x.detach().clone() for n, x in net.named_buffers()}
+    return dict(A=A.detach(), logits=logits.detach(), loss=loss.detach(), grads=grads, bufs=bufs)
+
+
 def tube_fixture(ref_model, name, b, t, seed_w=0):
-    from gen_golden_tube import run_reference_bf16_trunks as tube_bf16
 
     sd = tor.make_tube_state(seed_w, torch.float32)
     video = tor.make_video(b, t, 224)
@@ -143,6 +199,9 @@ def tube_fixture(ref_model, name, b, t, seed_w=0):
     }
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
+    for bn, (em, ev) in bn_stat_dev(rb["bufs"], bufs, TUBE_BUFS).items():
+        out["bf16ref_dev/bnstat/" + bn] = np.array([em, ev])
+        print(f"[{name}] bf16-trunk reference {bn}: batch-mean err {em:.2e} of std, batch-var rel err {ev:.2e}")
     print(f"[{name}] bf16-trunk reference deviation: " + ", ".join(
         f"{k}={np.max(v):.3e}" + (f" (median {np.median(v):.3e})" if np.ndim(v) else "") for k, v in dev.items()))
     out["video_checksum"] = checksum(video)

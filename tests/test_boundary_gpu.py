@@ -199,12 +199,26 @@ def test_grads_through_A_Pos_Neg_vs_oracle():
         assert abs(r - 1) <= max(5e-2, 3 * abs(rr - 1)), (n, r, rr)
 
 
+def _oracle_trunk_grads(sd, prefix, x, modal, R, bf16=False):
+    """The oracle trunk's layer4 map and the parameter gradients of <map, R> (bf16: CPU autocast)."""
+    leaves = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and k.startswith(prefix)
+                  and ("weight" in k or "bias" in k) else v.clone()) for k, v in sd.items()}
+    if bf16:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            y = orc.resnet18_forward(leaves, prefix, x, modal, training=True)
+        y = y.float()
+    else:
+        y = orc.resnet18_forward(leaves, prefix, x, modal, training=True)
+    (y * R.to(y.dtype)).sum().backward()
+    return y.detach(), {k: v.grad for k, v in leaves.items() if getattr(v, "grad", None) is not None}
+
+
 def test_standalone_trunks_forward_backward():
     """model.imgnet(x) and a standalone resnet18(modal='audio') (base_models.py:195-213): the layer4 map
-    and parameter gradients of <map, R> vs the fp64 oracle trunk."""
+    and parameter gradients of <map, R> vs the fp64 oracle trunk, within the deviation of the
+    oracle's own trunk in bf16 autocast (tiny fixture)."""
     img, aud = _tiny()
     model = _model()
-    sd = _sd64()
     for net, x, prefix, modal in ((model.imgnet, img, "imgnet.", "vision"), (None, aud, "audnet.", "audio")):
         if net is None:  # standalone, loaded from the audio trunk's weights
             torch.manual_seed(0)
@@ -212,22 +226,20 @@ def test_standalone_trunks_forward_backward():
             net.load_state_dict({k[len(prefix):]: v for k, v in orc.make_state(0).items() if k.startswith(prefix)})
             net = net.to(DEV).train()
         out = net(x.to(DEV))
-        ref_sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and ("weight" in k or "bias" in k)
-                      else v.clone()) for k, v in sd.items()}
-        ref = orc.resnet18_forward(ref_sd, prefix, x.double(), modal, training=True)
-        assert out.shape == ref.shape
-        e = rel_err(out, ref)
         g = torch.Generator().manual_seed(3)
-        R = torch.randn(ref.shape, generator=g)
+        R = torch.randn(out.shape, generator=g)
         (out * R.to(DEV)).sum().backward()
-        (ref * R.double()).sum().backward()
+        ref, g64 = _oracle_trunk_grads(_sd64(), prefix, x.double(), modal, R)
+        refb, gbf = _oracle_trunk_grads(orc.make_state(0), prefix, x, modal, R, bf16=True)
+        assert out.shape == ref.shape
+        e, eb = rel_err(out, ref), rel_err(refb, ref)
+        print(f"{modal}: map rel err {e:.3e} (bf16 reference {eb:.3e})")
+        assert e <= max(2e-2, 3 * eb)
         params = dict(net.named_parameters())
         for short in ["layer4.1.conv2.weight", "layer3.0.conv1.weight", "layer1.0.conv1.weight", "bn1.weight"]:
-            c = cosine(params[short].grad, ref_sd[prefix + short].grad)
-            print(f"{modal} {short}: cosine {c:.4f}")
-            assert c > 0.98, (modal, short, c)
-        print(f"{modal}: map rel err {e:.3e}")
-        assert e < 5e-2
+            c, cr = cosine(params[short].grad, g64[prefix + short]), cosine(gbf[prefix + short], g64[prefix + short])
+            print(f"{modal} {short}: cosine {c:.4f} (bf16 reference {cr:.4f})")
+            assert c >= min(0.98, 1 - 3 * (1 - cr)), (modal, short, c, cr)
         # the unused stems / fc never get a gradient
         assert params["conv1_flow.weight"].grad is None and params["fc.weight"].grad is None
 

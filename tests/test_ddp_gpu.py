@@ -2,7 +2,9 @@
 (RCCL needs one device per rank; the step's collective calls are backend-agnostic).
 
 Each rank runs HardWayTrainStep on its half of the batch with the bucketed, backward-overlapped
-gradient all-reduce (train.py), eager and then as captured segment graphs.  The parameters must
+gradient all-reduce (train.py: the two trunks concurrent on two HIP streams, the layer3+4 buckets of
+both issued between the two backward segments), eager and then as captured segment graphs; and with
+the single post-backward all-reduce.  The parameters must
 follow the single-process data-parallel update: Adam on the mean of the two local-negative
 gradients (nn.DataParallel semantics, train_hardway_1frame.py:93; model.py:114-115)."""
 import os
@@ -70,8 +72,8 @@ def _worker(rank, world, port, out_q, overlap):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("overlap", [False, True])
 def test_two_rank_allreduce_matches_dp_mean(overlap):
-    """overlap=False (default): concurrent-trunk graph + one all-reduce; True: bucketed all-reduces
-    overlapped with a sequential backward (segment graphs)."""
+    """overlap=True (default): bucketed all-reduces between the two concurrent-trunk backward segments
+    (two segment graphs); False: one graph + one all-reduce after the backward."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -97,7 +99,7 @@ def test_two_rank_allreduce_matches_dp_mean(overlap):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][2] == (4 if overlap else 0)  # imgnet hi/lo, audnet hi/lo segment graphs
+    assert res[0][2] == (2 if overlap else 0)  # fwd + layer4/3 backward of both trunks | layer2..stem
     # both ranks hold the same weights
     assert np.abs(res[0][1] - res[1][1]).max() == 0.0
 

@@ -13,8 +13,11 @@ HardWayTrainStep the bench times (eager, then replayed from its HIP graph).
 
 Tolerance = max(floor, 3 x the deviation of the REFERENCE's own trunks run under bf16 autocast with
 the fp32 head, measured at the same size by the generator) -- SURVEY §8(c)'s bf16 row, anchored as in
-test_model_gpu.py.  Running statistics: the implied batch mean within 2e-2 of the batch std and the
-implied unbiased batch variance within 2e-2 relative (bf16 conv operands, fp32/fp64 statistics).
+test_model_gpu.py.  Running statistics: the batch mean (error relative to the batch std) and the
+unbiased batch variance implied by the updated running_mean / running_var, each within
+max(5e-3, 3 x the bf16-autocast reference's own error) -- the stems' inputs round to bf16 before any
+statistic is taken (the spectrogram's narrow [-1.35, -0.6] range makes that 1-2 % of the audio
+stem's std in the reference's own bf16 run too).
 """
 import os
 
@@ -88,8 +91,11 @@ def _check_running_stats(g, sd, steps=1, tag=""):
         mean, var = rm / ak, (rv - 0.9 ** steps) / ak
         em = np.abs(mean - mean64).max() / np.sqrt(var64.max())
         ev = (np.abs(var - var64) / var64).max()
-        print(f"{tag} {bn}: batch-mean err {em:.2e} (of std), batch-var rel err {ev:.2e} over {len(rm)} channels")
-        assert em < 2e-2 and ev < 2e-2, (tag, bn, em, ev)
+        rm_ref, rv_ref = g["bf16ref_dev/bnstat/" + bn]
+        tm, tv = max(5e-3, 3 * rm_ref), max(5e-3, 3 * rv_ref)
+        print(f"{tag} {bn}: batch-mean err {em:.2e} of std (bf16 reference {rm_ref:.2e}, tol {tm:.2e}), "
+              f"batch-var rel err {ev:.2e} (bf16 reference {rv_ref:.2e}, tol {tv:.2e}) over {len(rm)} channels")
+        assert em <= tm and ev <= tv, (tag, bn, em, ev)
 
 
 def _avenet_inputs(g):

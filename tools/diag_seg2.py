@@ -1,4 +1,4 @@
-"""Segment-graph replay (HardWayTrainStep's world > 1 path: one HIP graph per gradient bucket) vs
+"""Segment-graph replay (HardWayTrainStep's world > 1 path: one HIP graph per backward segment) vs
 eager, on one process with the collectives stubbed out: relative gradient difference per bucket.
 This is how the hipMemsetAsync-node race in the head backward was found (garbage audio gradients
 in about half of the replays); keep it as a regression check of the segmented capture."""
@@ -22,8 +22,7 @@ def seg_vs_eager(B=2, seed=0):
     m.load_state_dict(orc.make_state(seed))
     m = m.to(dev).train()
     step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
-    step.world, step.overlap = 2, True  # take the segmented-capture path; collectives are no-ops
-    step.engine.concurrent = False
+    step.world, step.overlap = 2, True  # take the segmented-capture path (two streams); collectives are no-ops
     step._allreduce_bucket = lambda tag, works: None
     img, aud = orc.make_image(B, 64).to(dev), orc.make_spectrogram(B, 65, 76).to(dev)
     for _ in range(2):
