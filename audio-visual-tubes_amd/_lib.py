@@ -24,6 +24,13 @@ _L = ctypes.c_longlong
 _F = ctypes.c_float
 _Z = ctypes.c_size_t
 
+class DgradBnEpi(ctypes.Structure):
+    """avt_dgrad_bn_epi (include/avt.h): the BatchNorm-backward epilogue of avt_conv2d_dgrad_bn."""
+    _fields_ = [("xc", ctypes.c_void_p), ("y", ctypes.c_void_p), ("stats", ctypes.c_void_p),
+                ("acc", ctypes.c_void_p), ("xc2", ctypes.c_void_p), ("stats2", ctypes.c_void_p),
+                ("acc2", ctypes.c_void_p), ("skip_class00", ctypes.c_int)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
@@ -37,10 +44,13 @@ SIGNATURES = {
     "avt_set_nt128_config": (_I, [_I]),
     "avt_set_wgrad_slab_max": (_I, [_I, _I]),
     "avt_set_wgrad_tiles": (_I, [_I]),
+    "avt_set_small_tiles": (_I, [_I]),
     "avt_set_wgrad_halo": (_I, [_I]),
     "avt_bn_acc_doubles": (_Z, [_I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_conv2d_dgrad_bn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(DgradBnEpi), _P]),
+    "avt_bn_bwd_premasked": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),
     "avt_bn_finalize": (_I, [_P, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
@@ -90,7 +100,8 @@ _lock = threading.Lock()
 _lib = None
 
 
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared"]
+INCLUDE = os.path.join(os.path.dirname(PKG_DIR), "include")
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-shared"]
 HASH_PATH = LIB_PATH + ".sha256"
 
 
@@ -100,8 +111,8 @@ def source_hash() -> str:
     (a stale .so shipped with newer sources)."""
     import hashlib
 
-    h = hashlib.sha256(" ".join(HIPCC_FLAGS + SOURCES).encode())
-    inc = os.path.join(os.path.dirname(PKG_DIR), "include")
+    h = hashlib.sha256(" ".join([f for f in HIPCC_FLAGS if not f.startswith("-I")] + SOURCES).encode())
+    inc = INCLUDE
     files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
     if os.path.isdir(inc):
         files += sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h"))
@@ -126,13 +137,27 @@ def build(verbose: bool = False, force: bool = False) -> str:
     digest = source_hash()
     if not force and os.path.exists(LIB_PATH) and _recorded_hash() == digest:
         return LIB_PATH
-    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    import concurrent.futures
+    import tempfile
+
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB_PATH + ".tmp"
-    cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + srcs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True, cwd=CSRC)
+    with tempfile.TemporaryDirectory(prefix="avt_build_") as bdir:
+        def compile_one(src):
+            obj = os.path.join(bdir, os.path.splitext(src)[0] + ".o")
+            cmd = [hipcc] + HIPCC_FLAGS[:-1] + ["-c", os.path.join(CSRC, src), "-o", obj]  # no -shared
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True, cwd=CSRC)
+            return obj
+
+        jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+        with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(compile_one, SOURCES))
+        cmd = [hipcc] + HIPCC_FLAGS + ["-o", tmp] + objs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(tmp, LIB_PATH)
     with open(HASH_PATH, "w") as f:
         f.write(digest + "\n")

@@ -5,6 +5,8 @@
 #include <string.h>
 #include <stdio.h>
 
+#include "avt.h"  // (include/, -I) the C-ABI: every extern "C" definition must match its declaration
+
 typedef unsigned short bf16_t;  // storage type: raw bf16 bits
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

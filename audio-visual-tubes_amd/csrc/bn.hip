@@ -529,6 +529,28 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   return check_launch("bn_bwd");
 }
 
+// BN backward whose reductions were already accumulated into the workspace by a dgrad epilogue
+// (avt_conv2d_dgrad_bn) over the pre-masked g': finalize (dgamma, dbeta, k1, k2; re-zeroes the
+// accumulator) + apply gc = gamma*invstd*(g' - k1 - xhat*k2).  Same workspace contract as avt_bn_bwd.
+extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float* mean, const float* invstd,
+                                    const float* gamma, float* dgamma, float* dbeta, void* gc, void* workspace,
+                                    long long rows, int C, void* stream) {
+  AVT_REQUIRE(gm && xc && mean && invstd && gamma && gc && workspace, "bn_bwd_premasked: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn_bwd_premasked: C=%d unsupported", C);
+  AVT_REQUIRE(rows > 0, "bn_bwd_premasked: empty input");
+  AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_bwd_premasked: workspace must be 8-byte aligned");
+  double* acc = (double*)workspace;
+  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k2 = k1 + C;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
+  const long long nvec = rows * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)gm, nullptr,
+                     nullptr, nullptr, (const bf16_t*)xc, mean, invstd, gamma, k1, k2, (bf16_t*)gc, nullptr, nvec, C);
+  return check_launch("bn_bwd_premasked");
+}
+
 // BN + ReLU backward with the mask recomputed from the pre-activation xc and the forward's
 // (scale, shift): y is never read.  Same workspace contract as avt_bn_bwd.
 extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale, const float* shift,

@@ -33,6 +33,21 @@ struct GemmNTParams {
   int IT, OT;          // temporal extent of source / rows (Conv3d, temporal stride 1; 1 for Conv2d)
   int KT, pad_t;       // temporal taps and padding (Conv3d; 1 / 0 for Conv2d)
   int R, S, stride, pad;
+  // dgrad only -- fused BatchNorm-backward epilogue (conv_epi.h), active when bx != nullptr: the
+  // result g (after `add`) is masked by the ReLU of the BN that produced the positions' activations,
+  // g' = g * [by > 0] (by given: the block output) or g * [fma(bx, scale, shift) > 0] (BasicBlock.bn1),
+  // stored as g', and that BN's backward reductions (sum g', sum g' * xhat), xhat = (bx - mean)*invstd,
+  // are added (fp64 atomics) into bacc [AVT_BN_SLOTS][Ng][2]; bx2/bst2/bacc2 optionally a second BN fed
+  // by the same g' (the downsample BN of a first block: bn2 and downsample.1 share the ReLU).
+  const bf16_t* bx;
+  const bf16_t* by;
+  const float* bst;    // [4][Ng]: scale, shift, mean, invstd
+  double* bacc;
+  const bf16_t* bx2;
+  const float* bst2;
+  double* bacc2;
+  int bskip00;         // host side: a stride-2 dgrad's class-(0,0) launch stores plain g (another
+                       // kernel -- the downsample dgrad -- adds to those pixels and applies the epilogue)
 };
 
 __device__ __forceinline__ int swz64(int row, int chunk) {  // byte offset in a [rows][32 bf16] tile
@@ -456,6 +471,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
   }
 }
 
+#include "conv_epi.h"
 #include "conv_nt_pipe.h"
 #include "conv_tn_pipe.h"
 #include "conv_halo.h"
@@ -479,6 +495,7 @@ static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = 1;        // allow the 8-wave 256-wide wgrad tiles
+static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
                                    // measured 230-320 TFLOP/s vs 450-820 for the tap-gather kernel, see
                                    // conv_wgrad_halo.h)
@@ -555,6 +572,11 @@ extern "C" int avt_set_stem_kernel(int on) {
   return AVT_OK;
 }
 
+extern "C" int avt_set_small_tiles(int waves) {
+  avt::g_small_tile_waves = waves;
+  return AVT_OK;
+}
+
 extern "C" int avt_set_wgrad_tiles(int big) {
   avt::g_wgrad_big = big ? 1 : 0;
   return AVT_OK;
@@ -574,6 +596,9 @@ static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgsV& ta, hipStr
     if constexpr (MODE == MODE_FWD)
       hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK, true>), dim3(grid), dim3(WM * WN * 64), 0,
                          st, p, ta);
+  } else if (MODE == MODE_DGRAD && p.bx != nullptr) {
+    hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK, false, true>), dim3(grid),
+                       dim3(WM * WN * 64), 0, st, p, narrow_args(ta));
   } else {
     hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK>), dim3(grid), dim3(WM * WN * 64), 0, st, p,
                        narrow_args(ta));
@@ -624,6 +649,7 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
           ++tc.ntaps;
         }
       GemmNTParams pc = p;
+      if (p.bskip00 && ph == 0 && pw == 0) pc.bx = pc.bx2 = nullptr;
       pc.OH = (p.OH - ph + 1) / 2;
       pc.OW = (p.OW - pw + 1) / 2;
       pc.M = batch * pc.OH * pc.OW;
@@ -647,6 +673,23 @@ static bool halo_eligible(const GemmNTParams& p) {
   return p.Ng % 128 == 0 && 128 + 2 * p.OW + 2 <= 168;                                // W <= 19
 }
 
+// Small GEMMs (a few clips per GPU: BASELINE configs[2] runs 32 per GPU): a tile grid that leaves
+// most of the 256 CUs idle loses more than a smaller tile's lower reuse costs.  Rows per tile drop
+// from 128 to 64 when the 128-row grid would not give every CU `g_small_tile_waves` block(s)
+// (0 = never; env AVT_SMALL_TILES overrides the default 1, -1 = always).  Measured per shape
+// (tools/conv_bench.py --small): a 128-row grid of fewer blocks than CUs runs faster on 64-row tiles
+// (e.g. B=32 layer3 263 -> 354 TFLOP/s), one of 1-2 blocks per CU does not (B=32 audio layer4 769 -> 541).
+static bool use_small_tile(const GemmNTParams& p, int BN) {
+  if (g_small_tile_waves == -2) {
+    const char* e = getenv("AVT_SMALL_TILES");
+    g_small_tile_waves = e ? atoi(e) : 1;
+  }
+  if (g_small_tile_waves == 0) return false;
+  if (g_small_tile_waves < 0) return true;
+  const long long blocks128 = (long long)((p.M + 127) / 128) * (p.Ng / BN);
+  return blocks128 < (long long)g_small_tile_waves * num_cus();
+}
+
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR>
 static void launch_halo(const GemmNTParams& p, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -666,13 +709,28 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st) {
       ha.tap_w[t] = t;
     }
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
-  if (grid > 0)
+  if (grid > 0 && MODE == MODE_DGRAD && p.bx != nullptr)
+    hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>), dim3(grid), dim3(WM * WN * 64), 0,
+                       st, p, ha);
+  else if (grid > 0)
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX>), dim3(grid), dim3(WM * WN * 64), 0, st,
                        p, ha);
 }
 
 template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
+  if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && g_nt64_config == 1 &&
+      p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
+    if (p.Ng % 128 == 0) {
+      if (halo_eligible(p) && 64 + 2 * p.OW + 2 <= 104)
+        launch_halo<MODE, 2, 2, 1, 2, 2, 104>(p, st);  // 64 x 128 halo tile
+      else
+        launch_glds<MODE, 2, 2, 1, 2, 3>(p, st);  // 64 x 128, k32, 3 stages
+    } else {
+      launch_glds<MODE, 2, 2, 1, 1, 3>(p, st);  // 64 x 64, k32, 3 stages
+    }
+    return;
+  }
   if (CVEC == 8 && conv_variant() == 1 && halo_eligible(p)) {
     // measured (tools/conv_bench.py): the 4-wave 128 x 128 form at 2 blocks per CU beats the tap
     // gather on layer3/4 (W <= 19: +2..16 %); the 8-wave 256-row forms a patch of the wider layer1/2
@@ -754,13 +812,17 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
     sa.w = p.wmat;
     sa.y = p.out;
     sa.stats = bn_acc;
+    sa.N = N;
     sa.IH = H; sa.IW = W; sa.OH = p.OH; sa.OW = p.OW; sa.Kg = Kg;
-    sa.blocks_per_img = (p.OH * p.OW + kStemBM - 1) / kStemBM;
-    const dim3 grid(N * sa.blocks_per_img);
+    sa.chunks_per_img = (p.OH * p.OW + kStemCH - 1) / kStemCH;
+    sa.total_chunks = N * sa.chunks_per_img;
+    const int per_cu = Cp == 4 ? stem_blocks_per_cu<4>() : stem_blocks_per_cu<1>();
+    const int grid = sa.total_chunks < per_cu * num_cus() ? sa.total_chunks : per_cu * num_cus();
+    const size_t lds = Cp == 4 ? stem_lds_bytes<4>(p.OW) : stem_lds_bytes<1>(p.OW);
     if (Cp == 4)
-      hipLaunchKernelGGL(conv_stem_fwd_kernel<4>, grid, dim3(256), 0, st, sa);
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<4>, dim3(grid), dim3(512), lds, st, sa);
     else
-      hipLaunchKernelGGL(conv_stem_fwd_kernel<1>, grid, dim3(256), 0, st, sa);
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<1>, dim3(grid), dim3(512), lds, st, sa);
     return check_launch("conv2d_fwd (stem)");
   }
   const bool bn128 = (K % 128 == 0);
@@ -776,9 +838,14 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   return check_launch("conv2d_fwd");
 }
 
-extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C,
-                                int K, int R, int S, int stride, int pad, void* stream) {
+extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W,
+                                   int C, int K, int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi,
+                                   void* stream) {
   AVT_REQUIRE(dy && wt && dx, "conv2d_dgrad: null pointer");
+  AVT_REQUIRE(epi == nullptr || (epi->xc && epi->stats && epi->acc), "conv2d_dgrad: epilogue needs xc, stats, acc");
+  AVT_REQUIRE(epi == nullptr || epi->xc2 == nullptr || (epi->stats2 && epi->acc2),
+              "conv2d_dgrad: second BN needs stats2 and acc2");
+  AVT_REQUIRE(epi == nullptr || ((uintptr_t)epi->acc & 7) == 0, "conv2d_dgrad: acc must be 8-byte aligned");
   AVT_REQUIRE(C % 64 == 0 && K % 32 == 0, "conv2d_dgrad: C=%d K=%d unsupported", C, K);
   AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
   AVT_REQUIRE(R * S <= 32, "conv2d_dgrad: at most 32 taps");
@@ -800,12 +867,27 @@ extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const 
   p.Ng = C;
   p.Kg = R * S * K;
   p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  if (epi != nullptr) {
+    p.bx = (const bf16_t*)epi->xc;
+    p.by = (const bf16_t*)epi->y;
+    p.bst = epi->stats;
+    p.bacc = epi->acc;
+    p.bx2 = (const bf16_t*)epi->xc2;
+    p.bst2 = epi->stats2;
+    p.bacc2 = epi->acc2;
+    p.bskip00 = epi->skip_class00;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (C % 128 == 0)
     launch_nt<MODE_DGRAD, 8, 128, 128>(p, st);
   else
     launch_nt<MODE_DGRAD, 8, 128, 64>(p, st);
   return check_launch("conv2d_dgrad");
+}
+
+extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C,
+                                int K, int R, int S, int stride, int pad, void* stream) {
+  return avt_conv2d_dgrad_bn(dy, wt, dx, add, N, H, W, C, K, R, S, stride, pad, nullptr, stream);
 }
 
 // Conv3d forward (the R3D-18 video trunk, models/resnet3D.py:14-28 conv3x3x3 / conv1x1x1, called

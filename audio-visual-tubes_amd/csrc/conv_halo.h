@@ -26,7 +26,8 @@ struct HaloArgs {
 
 // WM x WN waves, each TM x TN 32x32 accumulators: BM = WM*TM*32 rows, BN = WN*TN*32 columns.
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX>
+// EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p, HaloArgs ha) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -272,23 +273,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
         Ct[r * CT_LD + cc] = f2bf(acc[i][j][v]);
       }
   __syncthreads();
-  constexpr int OCPR = BN / 8;
-  for (int idx = tid; idx < BM * OCPR; idx += NT) {
-    const int r = idx / OCPR, cc = idx - r * OCPR;
-    if (r >= rows_valid) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
-    const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
-    if (p.add != nullptr) {
-      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
-      unsigned* vv = reinterpret_cast<unsigned*>(&v);
-      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
-        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
-        vv[e] = pack2(lo, hi);
-      }
-    }
-    *reinterpret_cast<u32x4*>(p.out + off) = v;
-  }
+  epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, [&](int r) -> size_t { return (size_t)(m0 + r); },
+                        reinterpret_cast<float*>(smem));
 }

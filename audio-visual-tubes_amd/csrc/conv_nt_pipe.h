@@ -93,7 +93,8 @@ __device__ __forceinline__ int swz_rb(int row, int chunk) {
 // VID: rows carry a temporal coordinate and the tap list may exceed 32 taps (the Conv3d of the
 // R3D-18 video trunk and its 49-tap stem); the Conv2d instances keep the 32-bit mask and 2-D row
 // decode (measured: the general form costs the 2-D convs ~3.5 %).
-template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32, bool VID = false>
+// EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
+template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK = 32, bool VID = false, bool EPI = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     GemmNTParams p, typename std::conditional<VID, NTPipeArgsV, NTPipeArgs>::type ta) {
   typedef typename std::conditional<VID, unsigned long long, unsigned>::type mask_t;
@@ -338,30 +339,13 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
         Ct[r * CT_LD + c] = f2bf(acc[i][j][v]);
       }
   __syncthreads();
-  constexpr int OCPR = BN / 8;
-  for (int idx = tid; idx < BM * OCPR; idx += NT) {
-    const int r = idx / OCPR, cc = idx - r * OCPR;
-    if (r >= rows_valid) continue;
-    u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
-    size_t orow = (size_t)(m0 + r);
-    if (ta.cls) {  // class row -> full output pixel (2h'+ph, 2w'+pw)
-      const int m = m0 + r;
-      const int n = m / hw, rem = m - n * hw;
-      const int oh = rem / p.OW, ow = rem - oh * p.OW;
-      orow = ((size_t)n * ta.OHf + 2 * oh + ta.ph) * ta.OWf + 2 * ow + ta.pw;
-    }
-    const size_t off = orow * p.Ng + n0 + cc * 8;
-    if (p.add != nullptr) {
-      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
-      unsigned* vv = reinterpret_cast<unsigned*>(&v);
-      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
-        const float hi = bf2f(vv[e] >> 16) + bf2f(aa[e] >> 16);
-        vv[e] = pack2(lo, hi);
-      }
-    }
-    *reinterpret_cast<u32x4*>(p.out + off) = v;
-  }
+  // class mode: class row -> full output pixel (2h'+ph, 2w'+pw)
+  auto orow = [&](int r) -> size_t {
+    if (!ta.cls) return (size_t)(m0 + r);
+    const int m = m0 + r;
+    const int n = m / hw, rem = m - n * hw;
+    const int oh = rem / p.OW, ow = rem - oh * p.OW;
+    return ((size_t)n * ta.OHf + 2 * oh + ta.ph) * ta.OWf + 2 * ow + ta.pw;
+  };
+  epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, orow, reinterpret_cast<float*>(smem));
 }

@@ -1,204 +1,293 @@
 // 7x7 / stride 2 / pad 3 stem convolutions (models/base_models.py:135-138: the vision conv1 over
-// 3 channels padded to 4, the audio conv1_a over 1 channel), K = 64 output channels, forward with
-// the BN partial statistics of the other forward kernels.  Included by conv_gemm.hip inside
-// namespace avt (needs AVT_BN_SLOTS, f2bf).
+// 3 channels padded to 4, the audio conv1_a over 1 channel), 64 output channels, forward with the BN
+// partial statistics of the other forward kernels.  Included by conv_gemm.hip inside namespace avt
+// (needs AVT_BN_SLOTS, f2bf).
 //
-// The generic kernel gathers the stem's im2col one element at a time (C = 1 or 4 channels, 49 taps:
-// 86-212 TFLOP/s).  Here a block owns kStemBM = 512 consecutive output pixels of ONE image, copies
-// the input rows they read (with the 3-column padding) into an LDS patch once, and every A fragment
-// is read straight out of the patch:
-//   C = 4: k = (r*8 + s)*4 + c (a dummy 8th tap s = 7 with zero weight): a lane's 8 k values are
-//          taps (r, s0), (r, s0+1) x 4 channels = two adjacent patch pixels = one ds_read_b128;
-//          K = 7*8*4 = 224 (49*4 = 196 real), 14 MFMA k-steps.
-//   C = 1: k = r*8 + s (dummy tap s = 7, dummy row r = 7): a lane's 8 k values are one patch row's
-//          8 columns 2ow .. 2ow+7 = four ds_read_b32; K = 64 (49 real), 4 k-steps.
-// The weights are re-laid out into that k order in LDS as the block starts (from the packed
-// [64][Kg] operand of avt_pack_conv_weight, k = (r*7+s)*C + c).  4 waves x 128 rows (4 x 32-row
-// MFMA tiles) x 64 columns; epilogue: BN partial statistics per 128-row wave tile (sum, M2 about the
-// tile mean, sum^2/n: the format of the other conv epilogues), bf16 tile through LDS, 16-byte
-// coalesced stores.  Bound: the 2 B per output element store (205 MB vision, 317 MB audio at
-// B = 128) and the MFMA work of the padded K.
-// Measured on MI355X (tools/stem_ab.sh, B = 128 step): conv fwd 3.42 ms/step here vs 3.16 ms on the
-// generic kernel at 1 wave/SIMD (213 VGPR + 128 AGPR); with __launch_bounds__(256, 2) and the k loop
-// unrolled by 2 (220 VGPR, 2 blocks per CU) 3.35 vs 3.30 ms -- a tie, so it stays OFF by default
-// (AVT_STEM=1 / avt_set_stem_kernel(1) selects it).  What is left: one image per block leaves the
-// last block of each image partly idle (OH*OW % 512), and the LDS patch fill is serialised ahead of
-// the MFMA work (no double buffering) -- the store-bound floor (35-45 us per stem) is ~4x away.
+// The stem is store-bound: 1 input channel-group in, 64 bf16 channels out per output pixel (205 MB
+// vision / 317 MB audio at B = 128 against 51 / 20 MB of input), so the kernel is organised around
+// keeping the output stream going:
+//   * persistent: 512-thread blocks (8 waves) loop over 256-pixel chunks of one image (row-major
+//     output pixels), so the 64 x K weight operand goes to LDS once per block (kept in registers it
+//     spilled: 112 VGPRs of vision B fragments);
+//   * the chunk's input rows (its "patch": 2*(rows spanned - 1) + 7 input rows, the 3-column padding
+//     and out-of-image rows as zeros) sit in LDS, double-buffered: the next chunk's patch is loaded
+//     into registers while this chunk multiplies and written to the other buffer after it, one
+//     block barrier per chunk;
+//   * each wave owns one 32-pixel M tile of the chunk: A fragments straight out of the patch,
+//       C = 4: k = (r*8 + s)*4 + c (dummy tap s = 7, zero weight): a lane's 8 k values are taps
+//              (r, s0), (r, s0+1) x 4 channels = two adjacent patch pixels = one ds_read_b128;
+//              K = 224 (196 real), 14 MFMA k-steps;
+//       C = 1: k = r*8 + s (dummy row r = 7 and tap s = 7): a lane's 8 k values are 8 adjacent
+//              columns of one patch row = two ds_read2_b32; K = 64 (49 real), 4 k-steps;
+//   * epilogue per chunk and wave: BN statistics of the 32-row tile (sum, M2 about the tile mean)
+//     merged into per-lane running (n, sum, M2) in fp64 (Chan), the bf16 tile through the wave's own
+//     LDS region (no block barrier), four 16-byte stores per lane of the wave's contiguous 4 KB;
+//     at the end the 8 waves' statistics merge in LDS and each block adds (sum, M2, sum^2/n) into
+//     slot blockIdx % AVT_BN_SLOTS (the format avt_bn_finalize merges).
 #pragma once
 
 struct StemArgs {
   const bf16_t* x;  // [N][IH][IW][C]
-  const bf16_t* w;  // [64][Kg], k = (r*7+s)*C + c
+  const bf16_t* w;  // [64][Kg], k' = (r*7+s)*C + c
   bf16_t* y;        // [N][OH][OW][64]
   double* stats;    // optional [AVT_BN_SLOTS][64][3]
-  int IH, IW, OH, OW, Kg;
-  int blocks_per_img;
+  int N, IH, IW, OH, OW, Kg;
+  int chunks_per_img, total_chunks;
 };
 
-constexpr int kStemBM = 512;
-constexpr int kStemCT = 64 * 2 + 16;         // epilogue row pitch (bytes)
-constexpr int kStemLds = 4 * 128 * kStemCT;  // 72 KB: the epilogue tiles; 2 blocks per CU
+constexpr int kStemCH = 256;     // output pixels per chunk (8 waves x 32)
+constexpr int kStemCTP = 144;    // bytes per pixel row of a wave's staging tile (128 + 16 pad)
 
 template <int C>
 struct StemCfg {
-  static constexpr int KP = C == 4 ? 224 : 64;  // LDS k extent
-  static constexpr int KS = KP / 16;            // MFMA k-steps
-  static constexpr int BP = KP * 2 + 16;        // LDS weight row pitch (bytes)
+  static constexpr int KS = C == 4 ? 14 : 4;  // MFMA k-steps
+  static constexpr int MAXROWS = C == 4 ? 14 : 12;  // patch rows incl. one spare zero row
 };
 
+// patch geometry of a chunk
+struct StemChunk {
+  int img, p0, nvalid, oh_first, nrows;
+};
+
+__device__ __forceinline__ StemChunk stem_chunk(const StemArgs& a, int c) {
+  StemChunk k;
+  k.img = c / a.chunks_per_img;
+  const int blk = c - k.img * a.chunks_per_img;
+  const int P = a.OH * a.OW;
+  k.p0 = blk * kStemCH;
+  k.nvalid = min(kStemCH, P - k.p0);
+  k.oh_first = k.p0 / a.OW;
+  const int oh_last = (k.p0 + k.nvalid - 1) / a.OW;
+  k.nrows = 2 * (oh_last - k.oh_first) + 8;  // + a zero row (the C = 1 dummy row r = 7 reads it)
+  return k;
+}
+
 template <int C>
-__global__ __launch_bounds__(256, 2) void conv_stem_fwd_kernel(StemArgs a) {
+__global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
   using Cfg = StemCfg<C>;
-  constexpr int KS = Cfg::KS, BP = Cfg::BP;
-  __shared__ __attribute__((aligned(16))) char smem[kStemLds];
-  char* Bs = smem;            // [64][BP]
-  char* Ps = smem + 64 * BP;  // patch [nrows][PW][C] bf16
+  constexpr int KS = Cfg::KS, MAXROWS = Cfg::MAXROWS;
+  const int PW = 2 * a.OW + 6;         // patch columns: input x = -3 .. 2*OW + 2
+  const int ROWB = PW * C * 2;         // bytes per patch row
+  const int PATCHB = MAXROWS * ROWB;   // bytes per patch buffer
+  constexpr int KP = KS * 16, BP = KP * 2 + 16;  // weight rows: K bf16 + 16 B (bank spread)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Bs = smem;
+  char* patch[2] = {smem + 64 * BP, smem + 64 * BP + PATCHB};
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 31, fhalf = lane >> 5;
-  const int img = blockIdx.x / a.blocks_per_img, blk = blockIdx.x - img * a.blocks_per_img;
-  const int P = a.OH * a.OW;
-  const int p0 = blk * kStemBM;
-  const int oh_first = p0 / a.OW;
-  const int oh_last = (min(p0 + kStemBM, P) - 1) / a.OW;
-  const int nrows = 2 * (oh_last - oh_first) + 8;  // input rows 2*oh_first-3 ..; the last is a zero row
-  const int PW = 2 * a.OW + 6;                     // input columns -3 .. 2*OW+2
+  char* Ct = smem + 64 * BP + 2 * PATCHB + wid * 32 * kStemCTP;  // this wave's staging tile
 
-  // ---- weights -> LDS in the kernel's k order ----
-  if (C == 4) {
-    for (int u = tid; u < 64 * 56; u += 256) {  // (n, r, s) units of 4 channels = 8 bytes
-      const int n = u / 56, rs = u - n * 56, r = rs >> 3, s = rs & 7;
-      u32x2 v = {0u, 0u};
-      if (s < 7) v = *reinterpret_cast<const u32x2*>(a.w + (size_t)n * a.Kg + (r * 7 + s) * 4);
-      *reinterpret_cast<u32x2*>(Bs + n * BP + rs * 8) = v;
-    }
-  } else {
-    for (int u = tid; u < 64 * 64; u += 256) {
-      const int n = u >> 6, rs = u & 63, r = rs >> 3, s = rs & 7;
-      const bf16_t v = (r < 7 && s < 7) ? a.w[(size_t)n * a.Kg + r * 7 + s] : (bf16_t)0;
-      *reinterpret_cast<bf16_t*>(Bs + n * BP + rs * 2) = v;
-    }
-  }
-  // ---- input patch -> LDS (zeros outside the image and in the last row) ----
-  const bf16_t* xi = a.x + (size_t)img * a.IH * a.IW * C;
-  const int y0 = 2 * oh_first - 3;
-  for (int u = tid; u < nrows * PW; u += 256) {
-    const int g = u / PW, col = u - g * PW;
-    const int y = y0 + g, x = col - 3;
-    const bool ok = g < nrows - 1 && y >= 0 && y < a.IH && x >= 0 && x < a.IW;
+  // ---- weights -> LDS once per block, in the kernel's k order: Bs [64][KP + 8] bf16 ----
+  for (int u = tid; u < 64 * KP; u += 512) {
+    const int n = u / KP, k = u - n * KP;
+    int kp = -1;  // packed index (r*7+s)*C + c, or none (dummy tap / row)
     if (C == 4) {
-      u32x2 v = {0u, 0u};
-      if (ok) v = *reinterpret_cast<const u32x2*>(xi + ((size_t)y * a.IW + x) * 4);
-      *reinterpret_cast<u32x2*>(Ps + u * 8) = v;
+      const int rs = k >> 2, cc = k & 3, r = rs >> 3, s = rs & 7;
+      if (s < 7) kp = (r * 7 + s) * 4 + cc;
     } else {
-      *reinterpret_cast<bf16_t*>(Ps + u * 2) = ok ? xi[(size_t)y * a.IW + x] : (bf16_t)0;
+      const int r = k >> 3, s = k & 7;
+      if (r < 7 && s < 7) kp = r * 7 + s;
     }
+    *reinterpret_cast<bf16_t*>(Bs + n * BP + k * 2) = kp >= 0 ? a.w[(size_t)n * a.Kg + kp] : (bf16_t)0;
   }
-  __syncthreads();
 
-  // ---- per m-tile patch offset of this lane's pixel (rows past the image end: the last pixel) ----
-  int abase[4];
+  // ---- patch loads: thread t covers items t, t + 512, ... of (row, column) (C = 4: 8-B pixels) ----
+  constexpr int LPT = C == 4 ? 7 : 8;  // items per thread: 14 rows x 230 cols / 512; 12 x 306 / 512
+  typedef typename std::conditional<C == 4, u32x2, unsigned short>::type item_t;
+  item_t pre[LPT];
+  auto load_patch = [&](const StemChunk& k) {
+    const bf16_t* xi = a.x + (size_t)k.img * a.IH * a.IW * C;
+    const int y0 = 2 * k.oh_first - 3;
+    const int n_items = k.nrows * PW;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int p = min(p0 + wid * 128 + mt * 32 + frow, P - 1);
-    const int oh = p / a.OW, ow = p - oh * a.OW;
-    abase[mt] = ((2 * (oh - oh_first)) * PW + 2 * ow) * C * 2;
-  }
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-
-#pragma unroll 2
-  for (int ks = 0; ks < KS; ++ks) {
-    bf16x8 bfr[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (j * 32 + frow) * BP + (16 * ks + 8 * fhalf) * 2);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      bf16x8 af;
-      if (C == 4) {  // taps t0 = 4ks + 2fhalf, t0+1: row ks/2, columns s0, s0+1
-        const int off = ((ks >> 1) * PW + (4 * ks & 7) + 2 * fhalf) * 8;
-        af = *reinterpret_cast<const bf16x8*>(Ps + abase[mt] + off);
-      } else {  // row r = 2ks + fhalf, columns 0..7
-        const char* q = Ps + abase[mt] + (2 * ks + fhalf) * PW * 2;
-        u32x4 v;
-        v.x = *reinterpret_cast<const unsigned*>(q + 0);
-        v.y = *reinterpret_cast<const unsigned*>(q + 4);
-        v.z = *reinterpret_cast<const unsigned*>(q + 8);
-        v.w = *reinterpret_cast<const unsigned*>(q + 12);
-        af = __builtin_bit_cast(bf16x8, v);
+    for (int i = 0; i < LPT; ++i) {
+      const int u = tid + i * 512;
+      const int g = u / PW, col = u - g * PW;
+      const int yy = y0 + g, xx = col - 3;
+      const bool ok = u < n_items && g < k.nrows - 1 && yy >= 0 && yy < a.IH && xx >= 0 && xx < a.IW;
+      if constexpr (C == 4) {
+        pre[i] = ok ? *reinterpret_cast<const u32x2*>(xi + ((size_t)yy * a.IW + xx) * 4) : u32x2{0u, 0u};
+      } else {
+        pre[i] = ok ? xi[(size_t)yy * a.IW + xx] : (unsigned short)0;
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mt][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[j], acc[mt][j], 0, 0, 0);
     }
-  }
+  };
+  auto store_patch = [&](const StemChunk& k, char* dst) {
+    const int n_items = k.nrows * PW;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int u = tid + i * 512;
+      if (u < n_items) *reinterpret_cast<item_t*>(dst + (size_t)u * C * 2) = pre[i];
+    }
+  };
 
-  // ---- BN partial statistics of this wave's 128-row tile (fp32 results, before rounding) ----
-  const int rows_valid = min(128, P - (p0 + wid * 128));
-  if (a.stats != nullptr && rows_valid > 0) {
-    const size_t tile = ((size_t)img * a.blocks_per_img + blk) * 4 + wid;
-    double* slot = a.stats + (tile % AVT_BN_SLOTS) * 64 * 3;
+  // running BN statistics of this lane's two channels (j = 0, 1): rows n, sum, M2 about the mean
+  double st_n = 0.0, st_s[2] = {0.0, 0.0}, st_m2[2] = {0.0, 0.0};
+
+  int c = blockIdx.x;
+  StemChunk cur{};
+  if (c < a.total_chunks) {
+    cur = stem_chunk(a, c);
+    load_patch(cur);
+    store_patch(cur, patch[0]);
+  }
+  int buf = 0;
+  const int P = a.OH * a.OW;
+  for (; c < a.total_chunks; c += gridDim.x) {
+    __syncthreads();  // patch[buf] complete; every wave is past its reads of patch[buf ^ 1]
+    const int cn = c + gridDim.x;
+    StemChunk nxt{};
+    if (cn < a.total_chunks) {
+      nxt = stem_chunk(a, cn);
+      load_patch(nxt);  // in flight during this chunk's MFMAs
+    }
+    // ---- this wave's 32-pixel tile ----
+    const int row0 = wid * 32;  // first tile row within the chunk
+    const int rows_valid = min(32, cur.nvalid - row0);
+    if (rows_valid > 0) {
+      const int p = cur.p0 + row0 + min(frow, rows_valid - 1);  // clamp: tail rows compute a valid pixel
+      const int oh = p / a.OW, ow = p - oh * a.OW;
+      const char* pb = patch[buf] + (2 * (oh - cur.oh_first)) * ROWB + (2 * ow) * C * 2;
+      f32x16 acc[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float s = 0.f;
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+        for (int v = 0; v < 16; ++v) acc[j][v] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 af;
+        if constexpr (C == 4) {  // row ks/2, taps s0 = 4(ks&1) + 2 fhalf, s0 + 1
+          af = *reinterpret_cast<const bf16x8*>(pb + (ks >> 1) * ROWB + ((ks & 1) * 4 + 2 * fhalf) * 8);
+        } else {  // row 2 ks + fhalf, columns 0..7
+          const unsigned* q = reinterpret_cast<const unsigned*>(pb + (2 * ks + fhalf) * ROWB);
+          u32x4 v;
+          v.x = q[0];
+          v.y = q[1];
+          v.z = q[2];
+          v.w = q[3];
+          af = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 bf = *reinterpret_cast<const bf16x8*>(Bs + (j * 32 + frow) * BP + (16 * ks + 8 * fhalf) * 2);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[j], 0, 0, 0);
+        }
+      }
+      // ---- BN statistics of the tile (fp32 values before rounding), merged into the running ones ----
+      if (a.stats != nullptr) {
+        const double nt = (double)rows_valid;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float s = 0.f;
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+            if (r < rows_valid) s += acc[j][v];
+          }
+          s += __shfl_xor(s, 32, 64);
+          const float mean = s / (float)rows_valid;
+          float q = 0.f;
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+            const float d = acc[j][v] - mean;
+            if (r < rows_valid) q += d * d;
+          }
+          q += __shfl_xor(q, 32, 64);
+          // Chan: M2 += M2_t + (mean_t - mean)^2 * n * n_t / (n + n_t)
+          if (st_n > 0.0) {
+            const double d = (double)s / nt - st_s[j] / st_n;
+            st_m2[j] += (double)q + d * d * st_n * nt / (st_n + nt);
+          } else {
+            st_m2[j] += (double)q;
+          }
+          st_s[j] += (double)s;
+        }
+        st_n += nt;
+      }
+      // ---- bf16 tile through this wave's LDS region, then its contiguous 4 KB out ----
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-          const int r = mt * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-          if (r < rows_valid) s += acc[mt][j][v];
+          const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+          *reinterpret_cast<bf16_t*>(Ct + r * kStemCTP + (j * 32 + frow) * 2) = f2bf(acc[j][v]);
         }
-      s += __shfl_xor(s, 32, 64);
-      const float mean = s / (float)rows_valid;
-      float q = 0.f;
+      // a wave's LDS accesses complete in order: its own tile is read back without a barrier
+      bf16_t* yo = a.y + ((size_t)cur.img * P + cur.p0 + row0) * 64;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int r = mt * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-          const float d = acc[mt][j][v] - mean;
-          if (r < rows_valid) q += d * d;
-        }
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 32) {
-        double* c3 = slot + (size_t)(j * 32 + frow) * 3;
-        atomicAdd(c3 + 0, (double)s);
-        atomicAdd(c3 + 1, (double)q);
-        atomicAdd(c3 + 2, (double)s * (double)s / (double)rows_valid);
+      for (int i = 0; i < 4; ++i) {
+        const int u = lane + 64 * i;  // 256 chunks of 16 B: row u / 8, 16-B column u % 8
+        const int r = u >> 3, cc = u & 7;
+        if (r < rows_valid)
+          *reinterpret_cast<u32x4*>(yo + (size_t)r * 64 + cc * 8) =
+              *reinterpret_cast<const u32x4*>(Ct + r * kStemCTP + cc * 16);
       }
     }
+    if (cn < a.total_chunks) store_patch(nxt, patch[buf ^ 1]);
+    cur = nxt;
+    buf ^= 1;
   }
 
-  // ---- bf16 tile through LDS (each wave its own 128 x 64 region), 16-byte stores ----
-  __syncthreads();  // every wave is done with the patch and the weights
-  char* Ct = smem + wid * 128 * kStemCT;
+  // ---- merge the 8 waves' statistics (lanes < 32 hold channels j*32 + frow) and publish ----
+  if (a.stats != nullptr) {
+    __syncthreads();  // the patch buffers are free: reuse them
+    double* red = reinterpret_cast<double*>(smem + 64 * BP);  // [8 waves][64 ch][3]
+    if (lane < 32) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int r = mt * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-        *reinterpret_cast<bf16_t*>(Ct + r * kStemCT + (j * 32 + frow) * 2) = f2bf(acc[mt][j][v]);
+      for (int j = 0; j < 2; ++j) {
+        double* q = red + ((size_t)wid * 64 + j * 32 + frow) * 3;
+        q[0] = st_n;
+        q[1] = st_s[j];
+        q[2] = st_m2[j];
       }
-  // a wave's LDS accesses complete in issue order: its own tile is read back without a barrier
-  bf16_t* yo = a.y + ((size_t)img * P + p0 + wid * 128) * 64;
-  for (int u = lane; u < 128 * 8; u += 64) {
-    const int r = u >> 3, c = u & 7;
-    if (r < rows_valid)
-      *reinterpret_cast<u32x4*>(yo + (size_t)r * 64 + c * 8) =
-          *reinterpret_cast<const u32x4*>(Ct + r * kStemCT + c * 16);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      double n = 0.0, s = 0.0, m2 = 0.0;
+      for (int w = 0; w < 8; ++w) {
+        const double* q = red + ((size_t)w * 64 + tid) * 3;
+        const double nb = q[0];
+        if (nb <= 0.0) continue;
+        if (n > 0.0) {
+          const double d = q[1] / nb - s / n;
+          m2 += q[2] + d * d * n * nb / (n + nb);
+        } else {
+          m2 += q[2];
+        }
+        s += q[1];
+        n += nb;
+      }
+      if (n > 0.0) {
+        double* slot = a.stats + ((size_t)(blockIdx.x % AVT_BN_SLOTS) * 64 + tid) * 3;
+        atomicAdd(slot + 0, s);
+        atomicAdd(slot + 1, m2);
+        atomicAdd(slot + 2, s * s / n);
+      }
+    }
   }
 }
-
-// patch rows a block of kStemBM pixels can need (incl. the zero row)
-static inline int stem_patch_rows(int OW) { return 2 * ((kStemBM - 1) / OW + 1) + 8; }
 
 template <int C>
-static bool stem_fits(int OW) {
-  return 64 * StemCfg<C>::BP + (size_t)stem_patch_rows(OW) * (2 * OW + 6) * C * 2 <= (size_t)kStemLds;
+static size_t stem_lds_bytes(int OW) {
+  const size_t bs = (size_t)64 * (StemCfg<C>::KS * 16 * 2 + 16);
+  const size_t patchb = (size_t)StemCfg<C>::MAXROWS * (2 * OW + 6) * C * 2;
+  const size_t need = 2 * patchb + 8 * 32 * kStemCTP;
+  const size_t red = (size_t)8 * 64 * 3 * sizeof(double);
+  return bs + (need > red ? need : red);
 }
+
+// the chunk's rows must fit the patch: a 256-pixel chunk spans <= ceil(255 / OW) + 1 output rows
+template <int C>
+static bool stem_fits(int OW) {
+  const int rows_spanned = (kStemCH - 1) / OW + 2;
+  const int nrows = 2 * (rows_spanned - 1) + 8;
+  const int PW = 2 * OW + 6;
+  const int items_per_thread = C == 4 ? 7 : 8;
+  return OW >= 8 && nrows <= StemCfg<C>::MAXROWS && nrows * PW <= items_per_thread * 512 &&
+         stem_lds_bytes<C>(OW) <= 160 * 1024;
+}
+
+// blocks per CU of the persistent grid (~180 VGPRs: two waves per SIMD)
+template <int C>
+static int stem_blocks_per_cu() { return 1; }

@@ -412,18 +412,18 @@ class AVEngine:
                 ga = torch.empty_like(a)
                 call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
                      a.shape[1] * a.shape[2], C, stream_ptr())
-                ga = self.aud.backward_blocks(tape["aud"], ga, self.store, hi, len(self.aud.blocks))
+                ga, pa = self.aud.backward_blocks(tape["aud"], ga, self.store, hi, len(self.aud.blocks))
                 if not seg:
-                    ga = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi)
+                    ga, _ = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi, pa)
                     self.aud.backward_stem(tape["aud"], ga, self.store)
-            gv = self.img.backward_blocks(tape["img"], gv, self.store, hi, len(self.img.blocks))
+            gv, pv = self.img.backward_blocks(tape["img"], gv, self.store, hi, len(self.img.blocks))
             if seg:
                 self._join()
                 on_boundary((self.img.prefix + "hi", self.aud.prefix + "hi"))
                 with self._branch():  # second segment
-                    ga = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi)
+                    ga, _ = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi, pa)
                     self.aud.backward_stem(tape["aud"], ga, self.store)
-            gv = self.img.backward_blocks(tape["img"], gv, self.store, 0, hi)
+            gv, _ = self.img.backward_blocks(tape["img"], gv, self.store, 0, hi, pv)
             self.img.backward_stem(tape["img"], gv, self.store)
             self._join()
             if seg:

@@ -9,14 +9,18 @@ torch.bfloat16 tensors (raw bits shared with the kernels); BN statistics fp32.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import torch
 
-from ._lib import call, query
+from ._lib import DgradBnEpi, call, query
 
 STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
+# 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
+# reduce/apply passes of avt_bn_bwd (measured 1 % faster: DESIGN §6f)
+FUSE_BN_BWD = os.environ.get("AVT_FUSE_BN_BWD", "0") == "1"
 
 
 def P(t: Optional[torch.Tensor]):
@@ -278,14 +282,20 @@ class Trunk:
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
 
-    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False):
+    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False, epi=None):
         """inplace: accumulate into `add` (dx = add + dgrad); a strided 1x1 conv then only touches the
-        pixels its taps reach (the other parity classes of avt_conv2d_dgrad are skipped)."""
+        pixels its taps reach (the other parity classes of avt_conv2d_dgrad are skipped).
+        epi: DgradBnEpi -- the backward reductions of the BN+ReLU that produced dx's positions fused into
+        the store (dx = the masked gradient g'; avt_conv2d_dgrad_bn)."""
         _, wt = store.packed(spec)
         gx = add if inplace else torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
         ev = ConvProfiler.begin()
-        call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
-             spec.stride, spec.pad, stream_ptr())
+        if epi is None:
+            call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, stream_ptr())
+        else:
+            call("avt_conv2d_dgrad_bn", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, ctypes.byref(epi), stream_ptr())
         ConvProfiler.end(ev, "dgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (gy.numel() + wt.numel() + gx.numel() * (2 if add is not None else 1)))
         return gx
@@ -295,35 +305,80 @@ class Trunk:
     HI_BLOCK = 4  # index of layer3.0 in self.blocks
 
     def backward(self, tape: Dict, g_out: torch.Tensor, store: Store, on_boundary=None):
-        g = self.backward_blocks(tape, g_out, store, self.HI_BLOCK, len(self.blocks))
+        g, pm = self.backward_blocks(tape, g_out, store, self.HI_BLOCK, len(self.blocks))
         if on_boundary is not None:
             on_boundary(self.prefix + "hi")
-        g = self.backward_blocks(tape, g, store, 0, self.HI_BLOCK)
+        g, _ = self.backward_blocks(tape, g, store, 0, self.HI_BLOCK, pm)
         self.backward_stem(tape, g, store)
 
-    def backward_blocks(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int) -> torch.Tensor:
-        """Backward of blocks hi-1 .. lo (BasicBlock.forward, base_models.py:53-69); returns the gradient
-        of block lo's input."""
+    def _bn_bwd_premasked(self, gm, xc, stats, bn: BNSpec, store: Store):
+        """BN backward of a pre-masked g' whose reductions a dgrad epilogue already accumulated."""
+        gc = torch.empty_like(xc)
+        call("avt_bn_bwd_premasked", P(gm), P(xc), P(stats[2]), P(stats[3]), P(store.param(bn.prefix + ".weight")),
+             P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc),
+             P(store.stat_acc(bn, "bwd")), xc.numel() // bn.c, bn.c, stream_ptr())
+        return gc
+
+    def _epi(self, store: Store, bn: BNSpec, xc, stats, y=None, bn2: Optional[BNSpec] = None, xc2=None, stats2=None,
+             skip00: bool = False) -> DgradBnEpi:
+        e = DgradBnEpi()
+        e.xc, e.y, e.stats = xc.data_ptr(), (y.data_ptr() if y is not None else None), stats.data_ptr()
+        e.acc = store.stat_acc(bn, "bwd").data_ptr()
+        if bn2 is not None:
+            e.xc2, e.stats2, e.acc2 = xc2.data_ptr(), stats2.data_ptr(), store.stat_acc(bn2, "bwd").data_ptr()
+        e.skip_class00 = int(skip00)
+        return e
+
+    def backward_blocks(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int, premasked: bool = False):
+        """Backward of blocks hi-1 .. lo (BasicBlock.forward, base_models.py:53-69).  Returns (gradient of
+        block lo's input, premasked): with premasked the gradient is already multiplied by block lo-1's
+        output ReLU mask and that block's bn2 (+ downsample BN) reductions are accumulated -- each dgrad
+        that produces a BN's input gradient carries the BN-backward epilogue (avt_conv2d_dgrad_bn), so
+        the standalone reduction pass runs only where the gradient enters a trunk (from the head)."""
         N = tape["N"]
         for bi in reversed(range(lo, hi)):
             blk, t = self.blocks[bi], tape["blocks"][bi]
             Hc, Wc, Ho, Wo = t["H"], t["W"], t["Ho"], t["Wo"]
             identity = blk["down"] is None
-            gsum = torch.empty_like(t["c2"]) if identity else None
-            g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gsum)
-            self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
-            g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store)
-            g_c1 = self._bn_relu_bwd(g_h1, t["c1"], t["s1"], blk["bn1"], store)
-            self._wgrad(t["x"], g_c1, N, Hc, Wc, blk["conv1"], store)
-            if identity:
-                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=gsum)
+            if premasked:  # g = g' (masked), reductions already in the bn2 / downsample-BN accumulators
+                gres = g
+                g_c2 = self._bn_bwd_premasked(g, t["c2"], t["s2"], blk["bn2"], store)
+                g_cd = None if identity else self._bn_bwd_premasked(g, t["cd"], t["sd"], blk["bnd"], store)
             else:
-                g_cd = self._bn_bwd(g, t["out"], t["cd"], t["sd"], blk["bnd"], store)
+                gres = torch.empty_like(t["c2"]) if identity else None
+                g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gres)
+                g_cd = None if identity else self._bn_bwd(g, t["out"], t["cd"], t["sd"], blk["bnd"], store)
+            self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
+            if FUSE_BN_BWD:  # conv2 dgrad with bn1's backward (ReLU mask from its pre-activation) in the epilogue
+                g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store,
+                                   epi=self._epi(store, blk["bn1"], t["c1"], t["s1"]))
+                g_c1 = self._bn_bwd_premasked(g_h1, t["c1"], t["s1"], blk["bn1"], store)
+            else:
+                g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store)
+                g_c1 = self._bn_relu_bwd(g_h1, t["c1"], t["s1"], blk["bn1"], store)
+            self._wgrad(t["x"], g_c1, N, Hc, Wc, blk["conv1"], store)
+            if not identity:
                 self._wgrad(t["x"], g_cd, N, Hc, Wc, blk["down"], store)
-                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store)
-                g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True)
+            epi = None
+            if bi > 0 and FUSE_BN_BWD:  # the next block down: its bn2 (+ downsample BN) backward rides on this dgrad
+                pb, pt = self.blocks[bi - 1], tape["blocks"][bi - 1]
+                has_d = pb["down"] is not None
+                mk = lambda skip00: self._epi(store, pb["bn2"], pt["c2"], pt["s2"], y=pt["out"],
+                                              bn2=pb["bnd"] if has_d else None, xc2=pt["cd"] if has_d else None,
+                                              stats2=pt["sd"] if has_d else None, skip00=skip00)
+                epi = mk(False)
+            if identity:
+                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=gres, epi=epi)
+            else:
+                # the downsample dgrad (in place) finishes every pixel it reaches: the epilogue goes there;
+                # of a stride-2 conv1 dgrad only the (odd) pixels it alone writes carry it
+                strided = blk["conv1"].stride == 2
+                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store,
+                                  epi=mk(True) if (epi is not None and strided) else None)
+                g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True, epi=epi)
             g = g_x
-        return g
+            premasked = epi is not None
+        return g, premasked
 
     def backward_stem(self, tape: Dict, g: torch.Tensor, store: Store):
         """maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)."""

@@ -79,6 +79,10 @@ int avt_set_halo(int on);
  * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */
 int avt_set_nt128_config(int cfg);
+/* fwd/dgrad tiles of 64 rows (64x128 / 64x64; a 64x128 halo tile for layer3/4) when the 128-row tile
+ * grid would give fewer than `waves` blocks per CU (small per-GPU batches); 0 = never, -1 = always;
+ * default 1 (env AVT_SMALL_TILES) */
+int avt_set_small_tiles(int waves);
 /* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
  * at least min_ktiles 32-pixel tiles per block */
 int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
@@ -98,6 +102,25 @@ int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, in
 /* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
 int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, void* stream);
+/* avt_conv2d_dgrad with the backward of the BatchNorm (+ReLU) that produced dx's positions fused into
+ * its store epilogue (BasicBlock.forward, base_models.py:46-49, 58-67): the result g (after `add`) is
+ * masked, g' = g * [y > 0] (y given: the block output) or g * [fma(xc, scale, shift) > 0] (y NULL:
+ * BasicBlock.bn1's ReLU), dx = g' is stored, and sum g', sum g' * (xc - mean) * invstd are added into
+ * acc (the avt_bn_bwd workspace layout, [avt_bn_slots()][C][2] fp64); xc2/stats2/acc2 (optional) a
+ * second BN fed by the same g' (a first block's downsample.1).  skip_class00: for a stride-2 dgrad,
+ * the (even, even) pixels are stored plain (a later in-place downsample dgrad finishes them). */
+typedef struct {
+  const void* xc;      /* [N,H,W,C] bf16 pre-BN activations */
+  const void* y;       /* [N,H,W,C] bf16 ReLU output, or NULL */
+  const float* stats;  /* [4][C] fp32: scale, shift, mean, invstd (avt_bn_finalize outputs) */
+  double* acc;
+  const void* xc2;
+  const float* stats2;
+  double* acc2;
+  int skip_class00;
+} avt_dgrad_bn_epi;
+int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
+                        int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi, void* stream);
 /* dw[K][R][S][Creal] += wgrad(x[N,H,W,Cp], dy[N,P,Q,K]).  Split-K partials go through an fp32 slab
  * in `workspace` (>= avt_conv2d_wgrad_workspace(...) bytes; deterministic) or, if it is NULL/too
  * small or for the stems, are added with fp32 atomics. */
@@ -142,6 +165,10 @@ size_t avt_bn_bwd_workspace(long long rows, int C);
 int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
                const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out, void* workspace,
                long long rows, int C, void* stream);
+/* avt_bn_bwd for a g' that is already masked and whose reductions a dgrad epilogue already added
+ * into the workspace (avt_conv2d_dgrad_bn): finalize + apply only */
+int avt_bn_bwd_premasked(const void* gm, const void* xc, const float* mean, const float* invstd, const float* gamma,
+                         float* dgamma, float* dbeta, void* gc, void* workspace, long long rows, int C, void* stream);
 /* as avt_bn_bwd with g' = g*[fma(xc, scale, shift) > 0] -- the ReLU mask the forward's avt_bn_apply
  * produced from the same (scale, shift), recomputed instead of read */
 int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale, const float* shift, const float* mean,

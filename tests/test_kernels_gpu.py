@@ -94,8 +94,16 @@ def _rand_act(N, H, W, C, seed):
     return torch.randn(N, H, W, C, generator=g).to(torch.bfloat16)
 
 
+@pytest.fixture(params=[0, -1], ids=["tile128", "tile64"])
+def tiles(request):
+    """Run with the 128-row fwd/dgrad tiles, then with the 64-row small-batch tiles (avt_set_small_tiles)."""
+    call("avt_set_small_tiles", request.param)
+    yield request.param
+    call("avt_set_small_tiles", 1)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_and_bn_partials(case):
+def test_conv_fwd_and_bn_partials(case, tiles):
     N, H, W, C, K, R, st, pad = case
     x = _rand_act(N, H, W, C, 1).relu()
     g = torch.Generator().manual_seed(2)
@@ -203,9 +211,12 @@ def test_halo_matches_gather(case):
         torch.testing.assert_close(a1[:, 0], a0[:, 0], rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("cin,cp,H,W", [(3, 4, 20, 22), (1, 1, 21, 17), (3, 4, 224, 224), (1, 1, 257, 300)])
-def test_stem_fwd_wgrad(cin, cp, H, W):
-    N, K, R, st, pad = 2, 64, 7, 2, 3
+@pytest.mark.parametrize("cin,cp,H,W,N", [(3, 4, 20, 22, 2), (1, 1, 21, 17, 2), (3, 4, 224, 224, 2),
+                                           (1, 1, 257, 300, 2), (3, 4, 224, 224, 7), (1, 1, 257, 300, 16)])
+def test_stem_fwd_wgrad(cin, cp, H, W, N):
+    """Both stem forward kernels (the persistent LDS-patch one -- several chunks per block at the larger
+    N -- and the generic gather kernel) vs fp64, with their BN partial statistics; then the wgrad."""
+    K, R, st, pad = 64, 7, 2, 3
     g = torch.Generator().manual_seed(3)
     x = torch.randn(N, cin, H, W, generator=g)
     xd = x.to(DEV)
@@ -223,7 +234,7 @@ def test_stem_fwd_wgrad(cin, cp, H, W):
     n = rows.shape[0]
     outs = []
     try:
-        for stem_kernel in (1, 0):  # the LDS-patch stem kernel and the generic gather kernel (default)
+        for stem_kernel in (1, 0):  # the persistent LDS-patch stem kernel and the generic gather kernel
             call("avt_set_stem_kernel", stem_kernel)
             acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
             call("avt_conv2d_fwd", P(xn), P(wf), P(y), P(acc), N, H, W, cp, K, R, R, st, pad, kg, S())
@@ -248,7 +259,7 @@ def test_stem_fwd_wgrad(cin, cp, H, W):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_dgrad(case):
+def test_conv_dgrad(case, tiles):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     dy = _rand_act(N, Pq, Qq, K, 5)
@@ -639,3 +650,125 @@ def test_adam_matches_torch():
         call("avt_adam_step", P(pd), P(D(gr)), P(m), P(v), n, 1.0, 1e-3, 0.9, 0.999, 1e-8, 1e-4, t, S())
     torch.cuda.synchronize()
     assert rel_err(pd - p0.to(DEV), pr["p"] - p0.double()) < 1e-4
+
+
+def _dgrad_bn_ref(g, xc, stats, y=None):
+    """Reference of the fused BN-backward epilogue from the plain dgrad result g (bf16): the mask, the
+    masked gradient and the fp64 sums (sum g', sum g' * xhat) per channel."""
+    g, xc = g.double().cpu(), xc.double().cpu()
+    sc, sh, mean, inv = (stats[i].double().cpu() for i in range(4))
+    mask = (y.double().cpu() > 0) if y is not None else (xc.float() * sc.float() + sh.float() > 0)
+    gm = torch.where(mask, g, torch.zeros_like(g))
+    xhat = (xc - mean) * inv
+    C = g.shape[-1]
+    return gm, gm.reshape(-1, C).sum(0), (gm * xhat).reshape(-1, C).sum(0)
+
+
+def _bn_stats_rand(C, seed):
+    g = torch.Generator().manual_seed(seed)
+    sc = 1.0 + 0.2 * torch.randn(C, generator=g)
+    sh = 0.3 * torch.randn(C, generator=g)
+    mean = 0.1 * torch.randn(C, generator=g)
+    inv = 1.0 + 0.5 * torch.rand(C, generator=g)
+    return torch.stack([sc, sh, mean, inv]).float()
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("mode", ["relu_fma", "mask_y", "two_bn"])
+def test_conv_dgrad_bn_epilogue(case, mode):
+    """avt_conv2d_dgrad_bn: the store epilogue masks the dgrad result by the BN's ReLU (recomputed from
+    (xc, scale, shift) or read from y) and accumulates that BN's backward reductions (and a second
+    BN's) -- bitwise the masked plain-dgrad result, sums == fp64 sums of it; then
+    avt_bn_bwd_premasked consumes the accumulator like avt_bn_bwd."""
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    dy = _rand_act(N, Pq, Qq, K, 15)
+    g = torch.Generator().manual_seed(16)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float()
+    _, wt = pack(w.to(DEV), C, R * R * C)
+    add = _rand_act(N, H, W, C, 17) if mode != "two_bn" else None
+    plain = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    call("avt_conv2d_dgrad", P(D(dy)), P(wt), P(plain), P(D(add) if add is not None else None), N, H, W, C, K, R, R,
+         st, pad, S())
+    xc = _rand_act(N, H, W, C, 18)
+    stats = _bn_stats_rand(C, 19)
+    y = _rand_act(N, H, W, C, 20) if mode == "mask_y" else None
+    slots = int(query("avt_bn_slots"))
+    acc = torch.zeros(slots * C * 2 + C, device=DEV, dtype=torch.float64)
+    acc2 = torch.zeros_like(acc)
+    xc2, stats2 = _rand_act(N, H, W, C, 21), _bn_stats_rand(C, 22)
+    from avt_amd._lib import DgradBnEpi
+
+    e = DgradBnEpi()
+    e.xc, e.stats, e.acc = P(D(xc)).value, P(D(stats)).value, acc.data_ptr()
+    e.y = P(D(y)).value if y is not None else None
+    if mode == "two_bn":
+        e.xc2, e.stats2, e.acc2 = P(D(xc2)).value, P(D(stats2)).value, acc2.data_ptr()
+    dx = torch.empty_like(plain)
+    call("avt_conv2d_dgrad_bn", P(D(dy)), P(wt), P(dx), P(D(add) if add is not None else None), N, H, W, C, K, R, R,
+         st, pad, ctypes.byref(e), S())
+    torch.cuda.synchronize()
+    gm, s1, s2 = _dgrad_bn_ref(plain, xc, stats, y)
+    assert torch.equal(dx.cpu().double(), gm)
+    a = acc[: slots * C * 2].view(slots, C, 2).sum(0).cpu()
+    tol = 1e-5 * gm.abs().sum(0 if gm.dim() == 1 else tuple(range(gm.dim() - 1))).max().item() + 1e-6
+    np.testing.assert_allclose(a[:, 0].numpy(), s1.numpy(), atol=tol)
+    np.testing.assert_allclose(a[:, 1].numpy(), s2.numpy(), atol=tol * 4)
+    if mode == "two_bn":
+        _, s1b, s3 = _dgrad_bn_ref(plain, xc2, stats2, None)
+        b = acc2[: slots * C * 2].view(slots, C, 2).sum(0).cpu()
+        np.testing.assert_allclose(b[:, 0].numpy(), s1.numpy(), atol=tol)  # sum g' of the FIRST BN's mask
+        xh2 = (xc2.double() - stats2[2].double()) * stats2[3].double()
+        np.testing.assert_allclose(b[:, 1].numpy(), (gm * xh2).reshape(-1, C).sum(0).numpy(), atol=tol * 4)
+    # premasked finalize + apply == the reference BN backward on g'
+    gamma = (1.0 + 0.1 * torch.randn(C, generator=g)).float().to(DEV)
+    dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    gc = torch.empty_like(dx)
+    rows = N * H * W
+    call("avt_bn_bwd_premasked", P(dx), P(D(xc)), P(D(stats[2])), P(D(stats[3])), P(gamma), P(dgamma), P(dbeta), P(gc),
+         P(acc), rows, C, S())
+    torch.cuda.synchronize()
+    assert acc[: slots * C * 2].abs().max().item() == 0.0  # consumed and re-zeroed
+    xhat = (xc.double() - stats[2].double()) * stats[3].double()
+    k1, k2 = s1 / rows, s2 / rows
+    ref_gc = gamma.double().cpu() * stats[3].double() * (gm - k1 - xhat * k2)
+    assert rel_err(gc, ref_gc) < 8e-3
+    np.testing.assert_allclose(dbeta.cpu().double().numpy(), s1.numpy(), atol=tol)
+    np.testing.assert_allclose(dgamma.cpu().double().numpy(), s2.numpy(), atol=tol * 4)
+
+
+@pytest.mark.parametrize("case", [(2, 9, 11, 64, 128, 3, 2, 1), (2, 15, 13, 64, 128, 3, 2, 1)])
+def test_strided_dgrad_skip00_then_downsample_epilogue(case):
+    """A first block's input gradient: the 3x3/s2 conv1 dgrad stores its class-(0,0) pixels plain
+    (skip_class00), the in-place 1x1/s2 downsample dgrad adds to them and applies the epilogue: the
+    union equals the masked sum of both dgrads, the sums cover every pixel once."""
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, 3, 2, 1), conv_out(W, 3, 2, 1)
+    dy1, dyd = _rand_act(N, Pq, Qq, K, 25), _rand_act(N, Pq, Qq, K, 26)
+    g = torch.Generator().manual_seed(27)
+    w1 = (torch.randn(K, 3, 3, C, generator=g) * 0.05).float()
+    wd = (torch.randn(K, 1, 1, C, generator=g) * 0.05).float()
+    _, wt1 = pack(w1.to(DEV), C, 9 * C)
+    _, wtd = pack(wd.to(DEV), C, C)
+    ref = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    call("avt_conv2d_dgrad", P(D(dy1)), P(wt1), P(ref), None, N, H, W, C, K, 3, 3, 2, 1, S())
+    call("avt_conv2d_dgrad", P(D(dyd)), P(wtd), P(ref), P(ref), N, H, W, C, K, 1, 1, 2, 0, S())
+    xc, y, stats = _rand_act(N, H, W, C, 28), _rand_act(N, H, W, C, 29), _bn_stats_rand(C, 30)
+    slots = int(query("avt_bn_slots"))
+    acc = torch.zeros(slots * C * 2 + C, device=DEV, dtype=torch.float64)
+    from avt_amd._lib import DgradBnEpi
+
+    e = DgradBnEpi()
+    e.xc, e.y, e.stats, e.acc = P(D(xc)).value, P(D(y)).value, P(D(stats)).value, acc.data_ptr()
+    e.skip_class00 = 1
+    dx = torch.empty_like(ref)
+    call("avt_conv2d_dgrad_bn", P(D(dy1)), P(wt1), P(dx), None, N, H, W, C, K, 3, 3, 2, 1, ctypes.byref(e), S())
+    e.skip_class00 = 0
+    call("avt_conv2d_dgrad_bn", P(D(dyd)), P(wtd), P(dx), P(dx), N, H, W, C, K, 1, 1, 2, 0, ctypes.byref(e), S())
+    torch.cuda.synchronize()
+    gm, s1, s2 = _dgrad_bn_ref(ref, xc, stats, y)
+    assert torch.equal(dx.cpu().double(), gm)
+    a = acc[: slots * C * 2].view(slots, C, 2).sum(0).cpu()
+    tol = 1e-5 * gm.abs().sum((0, 1, 2)).max().item() + 1e-6
+    np.testing.assert_allclose(a[:, 0].numpy(), s1.numpy(), atol=tol)
+    np.testing.assert_allclose(a[:, 1].numpy(), s2.numpy(), atol=tol * 4)
