@@ -19,8 +19,9 @@
 //              K = 224 (196 real), 14 MFMA k-steps;
 //       C = 1: k = r*8 + s (dummy row r = 7 and tap s = 7): a lane's 8 k values are 8 adjacent
 //              columns of one patch row = two ds_read2_b32; K = 64 (49 real), 4 k-steps;
-//   * epilogue per chunk and wave: BN statistics of the 32-row tile (sum, M2 about the tile mean)
-//     merged into per-lane running (n, sum, M2) in fp64 (Chan), the bf16 tile through the wave's own
+//   * epilogue per chunk and wave: BN statistics of the 32-row tile (sum, and sum of squares about a
+//     per-channel shift = the wave's first tile mean) accumulated per lane in fp64 -- no division in
+//     the loop; M2 = Q - (S - n shift)^2 / n once at the end --, the bf16 tile through the wave's own
 //     LDS region (no block barrier), four 16-byte stores per lane of the wave's contiguous 4 KB;
 //     at the end the 8 waves' statistics merge in LDS and each block adds (sum, M2, sum^2/n) into
 //     slot blockIdx % AVT_BN_SLOTS (the format avt_bn_finalize merges).
@@ -72,7 +73,9 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
   constexpr int KP = KS * 16, BP = KP * 2 + 16;  // weight rows: K bf16 + 16 B (bank spread)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Bs = smem;
-  char* patch[2] = {smem + 64 * BP, smem + 64 * BP + PATCHB};
+  char* const patch0 = smem + 64 * BP;  // patch buffer b at patch0 + b * PATCHB (pointer arithmetic on
+                                        // smem: an array of LDS pointers indexed at run time lowered
+                                        // the fragment reads to flat loads)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 31, fhalf = lane >> 5;
   char* Ct = smem + 64 * BP + 2 * PATCHB + wid * 32 * kStemCTP;  // this wave's staging tile
@@ -121,15 +124,19 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
     }
   };
 
-  // running BN statistics of this lane's two channels (j = 0, 1): rows n, sum, M2 about the mean
-  double st_n = 0.0, st_s[2] = {0.0, 0.0}, st_m2[2] = {0.0, 0.0};
+  // running BN statistics of this lane's two channels (j = 0, 1): rows n, sum, and the sum of squares
+  // about a per-channel shift (the first tile's mean) -- no division in the chunk loop; the M2 about
+  // the running mean is recovered once at the end (shifted-data variance)
+  double st_n = 0.0, st_s[2] = {0.0, 0.0}, st_q[2] = {0.0, 0.0};
+  float shift[2] = {0.f, 0.f};
+  bool have_shift = false;
 
   int c = blockIdx.x;
   StemChunk cur{};
   if (c < a.total_chunks) {
     cur = stem_chunk(a, c);
     load_patch(cur);
-    store_patch(cur, patch[0]);
+    store_patch(cur, patch0);
   }
   int buf = 0;
   const int P = a.OH * a.OW;
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
     if (rows_valid > 0) {
       const int p = cur.p0 + row0 + min(frow, rows_valid - 1);  // clamp: tail rows compute a valid pixel
       const int oh = p / a.OW, ow = p - oh * a.OW;
-      const char* pb = patch[buf] + (2 * (oh - cur.oh_first)) * ROWB + (2 * ow) * C * 2;
+      const char* pb = patch0 + buf * PATCHB + (2 * (oh - cur.oh_first)) * ROWB + (2 * ow) * C * 2;
       f32x16 acc[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -173,38 +180,45 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[j], 0, 0, 0);
         }
       }
-      // ---- BN statistics of the tile (fp32 values before rounding), merged into the running ones ----
+      // ---- BN statistics of the tile (fp32 values before rounding): sum and sum of squares about the
+      //      channel's shift, accumulated in fp64 ----
       if (a.stats != nullptr) {
-        const double nt = (double)rows_valid;
+        if (!have_shift) {  // first tile of this wave: its mean becomes the shift
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float sm = 0.f;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+              const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+              if (r < rows_valid) sm += acc[j][v];
+            }
+            sm += __shfl_xor(sm, 32, 64);
+            shift[j] = sm / (float)rows_valid;
+          }
+          have_shift = true;
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          float s = 0.f;
+          float sm = 0.f, q = 0.f;
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
             const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-            if (r < rows_valid) s += acc[j][v];
+            const float d = acc[j][v] - shift[j];
+            if (r < rows_valid) {
+              sm += acc[j][v];
+              q += d * d;
+            }
           }
-          s += __shfl_xor(s, 32, 64);
-          const float mean = s / (float)rows_valid;
-          float q = 0.f;
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int r = (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-            const float d = acc[j][v] - mean;
-            if (r < rows_valid) q += d * d;
-          }
+          sm += __shfl_xor(sm, 32, 64);
           q += __shfl_xor(q, 32, 64);
-          // Chan: M2 += M2_t + (mean_t - mean)^2 * n * n_t / (n + n_t)
-          if (st_n > 0.0) {
-            const double d = (double)s / nt - st_s[j] / st_n;
-            st_m2[j] += (double)q + d * d * st_n * nt / (st_n + nt);
-          } else {
-            st_m2[j] += (double)q;
-          }
-          st_s[j] += (double)s;
+          st_s[j] += (double)sm;
+          st_q[j] += (double)q;
         }
-        st_n += nt;
+        st_n += (double)rows_valid;
       }
+      // the next chunk's patch goes to LDS now, before this tile's stores: its wait for the
+      // prefetch loads then does not also wait for the output stores (vmcnt counts both, in order)
+      if (cn < a.total_chunks) store_patch(nxt, patch0 + (buf ^ 1) * PATCHB);
       // ---- bf16 tile through this wave's LDS region, then its contiguous 4 KB out ----
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -223,8 +237,9 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
           *reinterpret_cast<u32x4*>(yo + (size_t)r * 64 + cc * 8) =
               *reinterpret_cast<const u32x4*>(Ct + r * kStemCTP + cc * 16);
       }
+    } else if (cn < a.total_chunks) {
+      store_patch(nxt, patch0 + (buf ^ 1) * PATCHB);
     }
-    if (cn < a.total_chunks) store_patch(nxt, patch[buf ^ 1]);
     cur = nxt;
     buf ^= 1;
   }
@@ -237,9 +252,11 @@ __global__ __launch_bounds__(512, 2) void conv_stem_fwd_kernel(StemArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         double* q = red + ((size_t)wid * 64 + j * 32 + frow) * 3;
+        // M2 about this wave's mean: Q - (S - n c)^2 / n
+        const double dc = st_n > 0.0 ? st_s[j] - st_n * (double)shift[j] : 0.0;
         q[0] = st_n;
         q[1] = st_s[j];
-        q[2] = st_m2[j];
+        q[2] = st_n > 0.0 ? fmax(st_q[j] - dc * dc / st_n, 0.0) : 0.0;
       }
     }
     __syncthreads();
