@@ -41,6 +41,7 @@ SIGNATURES = {
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
     "avt_set_stem_kernel": (_I, [_I]),
+    "avt_set_stem_wgrad": (_I, [_I]),
     "avt_set_nt128_config": (_I, [_I]),
     "avt_set_wgrad_slab_max": (_I, [_I, _I]),
     "avt_set_wgrad_tiles": (_I, [_I]),

@@ -477,15 +477,25 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_halo.h"
 #include "conv_wgrad_halo.h"
 #include "conv_stem.h"
+#include "conv_stem_wgrad.h"
 
-static int g_stem_kernel = -1;  // 7x7/s2 stems on conv_stem_fwd_kernel: -1 = env AVT_STEM (default 0, the
-                                // generic gather kernel: measured 0.25 ms/step faster at B=128, conv_stem.h)
+static int g_stem_kernel = -1;  // 7x7/s2 stem forwards on conv_stem_fwd_kernel: -1 = env AVT_STEM (default 1;
+                                // 0 = the generic gather kernel, ~1.7x slower: tools/stem_bench.py)
 static int stem_enabled() {
   if (g_stem_kernel < 0) {
     const char* e = getenv("AVT_STEM");
-    g_stem_kernel = e ? atoi(e) : 0;
+    g_stem_kernel = e ? atoi(e) : 1;
   }
   return g_stem_kernel;
+}
+
+static int g_stem_wgrad = -1;  // 7x7/s2 stem wgrads on conv_stem_wgrad_kernel: -1 = env AVT_STEM_WGRAD (default 1)
+static int stem_wgrad_enabled() {
+  if (g_stem_wgrad < 0) {
+    const char* e = getenv("AVT_STEM_WGRAD");
+    g_stem_wgrad = e ? atoi(e) : 1;
+  }
+  return g_stem_wgrad;
 }
 
 static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
@@ -564,6 +574,11 @@ extern "C" int avt_set_wgrad_slab_max(int max_splits, int wave_cost) {
   AVT_REQUIRE(max_splits >= 0 && wave_cost >= 0, "set_wgrad_slab_max: bad arguments");
   avt::g_wgrad_slab_max = max_splits;
   avt::g_wgrad_wave_cost = wave_cost;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_stem_wgrad(int on) {
+  avt::g_stem_wgrad = on ? 1 : 0;
   return AVT_OK;
 }
 
@@ -812,17 +827,19 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
     sa.w = p.wmat;
     sa.y = p.out;
     sa.stats = bn_acc;
+    sa.x_bytes = (unsigned)((size_t)N * H * W * Cp * 2);
+    sa.y_bytes = (unsigned)((size_t)p.M * K * 2);
     sa.N = N;
     sa.IH = H; sa.IW = W; sa.OH = p.OH; sa.OW = p.OW; sa.Kg = Kg;
-    sa.chunks_per_img = (p.OH * p.OW + kStemCH - 1) / kStemCH;
-    sa.total_chunks = N * sa.chunks_per_img;
-    const int per_cu = Cp == 4 ? stem_blocks_per_cu<4>() : stem_blocks_per_cu<1>();
-    const int grid = sa.total_chunks < per_cu * num_cus() ? sa.total_chunks : per_cu * num_cus();
-    const size_t lds = Cp == 4 ? stem_lds_bytes<4>(p.OW) : stem_lds_bytes<1>(p.OW);
+    sa.tiles_per_row = (p.OW + 31) / 32;
+    sa.total_tiles = N * p.OH * sa.tiles_per_row;
+    const int blocks = (sa.total_tiles + kStemNW - 1) / kStemNW;  // kStemNW wave tiles per block round
+    const int grid = blocks < num_cus() ? blocks : num_cus();
+    const size_t lds = Cp == 4 ? stem_lds_bytes<4>() : stem_lds_bytes<1>();
     if (Cp == 4)
-      hipLaunchKernelGGL(conv_stem_fwd_kernel<4>, dim3(grid), dim3(512), lds, st, sa);
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<4>, dim3(grid), dim3(kStemNW * 64), lds, st, sa);
     else
-      hipLaunchKernelGGL(conv_stem_fwd_kernel<1>, dim3(grid), dim3(512), lds, st, sa);
+      hipLaunchKernelGGL(conv_stem_fwd_kernel<1>, dim3(grid), dim3(kStemNW * 64), lds, st, sa);
     return check_launch("conv2d_fwd (stem)");
   }
   const bool bn128 = (K % 128 == 0);
@@ -1149,8 +1166,36 @@ extern "C" int avt_set_wgrad_halo(int on) {
   return AVT_OK;
 }
 
+namespace avt {
+// stem wgrad on conv_stem_wgrad_kernel: grid (one block per CU at most) and its slab bytes; grid 0 = n/a
+struct StemWgradPlan {
+  int grid = 0;
+  size_t slab_bytes = 0;
+  StemWgradArgs a{};
+};
+static StemWgradPlan stem_wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
+  StemWgradPlan pl;
+  if (!((Cp == 4 || Cp == 1) && stem_wgrad_enabled() && K == 64 && R == 7 && S == 7 && stride == 2 && pad == 3 &&
+        Creal >= 1 && Creal <= Cp && N >= 1))
+    return pl;
+  const int OH = (H + 2 * pad - R) / stride + 1, OW = (W + 2 * pad - S) / stride + 1;
+  if (OH < 1 || OW < 1) return pl;
+  if ((size_t)N * H * W * Cp * 2 >= (1ull << 31) || (size_t)N * OH * OW * 64 * 2 >= (1ull << 31)) return pl;  // 32-bit offsets
+  pl.a.N = N; pl.a.IH = H; pl.a.IW = W; pl.a.OH = OH; pl.a.OW = OW; pl.a.Creal = Creal;
+  pl.a.tiles_per_row = (OW + 31) / 32;
+  pl.a.total_tiles = N * OH * pl.a.tiles_per_row;
+  const int nw = Cp == 4 ? StemWgradCfg<4>::NW : StemWgradCfg<1>::NW;
+  const int blocks = (pl.a.total_tiles + nw - 1) / nw;
+  pl.grid = blocks < num_cus() ? blocks : num_cus();
+  pl.slab_bytes = (size_t)pl.grid * 64 * 49 * Creal * sizeof(float);
+  return pl;
+}
+}  // namespace avt
+
 extern "C" size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride,
                                              int pad) {
+  const StemWgradPlan sp = stem_wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  if (sp.grid > 0) return sp.slab_bytes;
   const WgradHaloPlan hp = wgrad_halo_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
   if (hp.ok) return hp.slab_bytes;
   return wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad).slab_bytes;
@@ -1167,6 +1212,25 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
   AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
   AVT_REQUIRE(Creal <= Cp, "conv2d_wgrad: Creal > Cp");
   AVT_REQUIRE(Cp % 8 != 0 || Creal == Cp, "conv2d_wgrad: channel padding only for the stems");
+  StemWgradPlan sp = stem_wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  if (sp.grid > 0 && workspace != nullptr && ws_bytes >= sp.slab_bytes) {
+    sp.a.x = (const bf16_t*)x;
+    sp.a.dy = (const bf16_t*)dy;
+    sp.a.slab = (float*)workspace;
+    sp.a.x_bytes = (unsigned)((size_t)N * H * W * Cp * 2);
+    sp.a.dy_bytes = (unsigned)((size_t)N * sp.a.OH * sp.a.OW * 64 * 2);
+    hipStream_t st = (hipStream_t)stream;
+    if (Cp == 4)
+      hipLaunchKernelGGL(conv_stem_wgrad_kernel<4>, dim3(sp.grid), dim3(StemWgradCfg<4>::NW * 64),
+                         stem_wgrad_lds_bytes<4>(), st, sp.a);
+    else
+      hipLaunchKernelGGL(conv_stem_wgrad_kernel<1>, dim3(sp.grid), dim3(StemWgradCfg<1>::NW * 64),
+                         stem_wgrad_lds_bytes<1>(), st, sp.a);
+    const int n = 64 * 49 * Creal;
+    hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((n + 63) / 64), dim3(1024), 0, st, (const float*)workspace,
+                       sp.grid, n, dw);
+    return check_launch("conv2d_wgrad(stem)");
+  }
   WgradHaloPlan hp = wgrad_halo_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
   if (hp.ok) {
     // without the workspace the split partials are added with fp32 atomics

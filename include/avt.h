@@ -93,9 +93,12 @@ int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 int avt_set_wgrad_tiles(int big);
 /* 3x3/s1 wgrads on the halo-reuse kernel (1; env AVT_WGRAD_HALO) or the tap-gather one (0, default) */
 int avt_set_wgrad_halo(int on);
-/* 1: the 7x7/s2 stems (C 4 or 1, K 64) run on the LDS-patch stem kernel; 0 (default, env AVT_STEM):
- * the generic gather kernel, measured faster in the B=128 step — an A/B knob */
+/* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
+ * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */
 int avt_set_stem_kernel(int on);
+/* 1 (default, env AVT_STEM_WGRAD): the 7x7/s2 stem wgrads (C 4 or 1, K 64) run on the per-wave
+ * LDS-patch kernel (needs the avt_conv2d_wgrad_workspace() slab; deterministic); 0: the generic one */
+int avt_set_stem_wgrad(int on);
 size_t avt_bn_acc_doubles(int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);

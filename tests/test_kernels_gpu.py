@@ -241,21 +241,35 @@ def test_stem_fwd_wgrad(cin, cp, H, W, N):
             torch.cuda.synchronize()
             assert rel_err(y, ref) < 8e-3, stem_kernel
             a = acc.view(-1, K, 3).sum(0).cpu()
-            np.testing.assert_allclose(a[:, 0].numpy(), rows.sum(0).numpy(), rtol=1e-4,
-                                       atol=1e-4 * rows.abs().max().item() * n ** 0.5)
+            # the stem kernel takes the statistics of the bf16 tensor it stores (on the MFMA pipe,
+            # conv_stem.h), the generic kernel those of the fp32 values before rounding
+            srows = y.reshape(-1, K).double().cpu() if stem_kernel else rows
+            np.testing.assert_allclose(a[:, 0].numpy(), srows.sum(0).numpy(), rtol=1e-4,
+                                       atol=1e-4 * srows.abs().max().item() * n ** 0.5)
             m2 = a[:, 1] + a[:, 2] - a[:, 0] ** 2 / n
-            np.testing.assert_allclose(m2.numpy(), ((rows - rows.mean(0)) ** 2).sum(0).numpy(), rtol=1e-4)
+            np.testing.assert_allclose(m2.numpy(), ((srows - srows.mean(0)) ** 2).sum(0).numpy(), rtol=1e-4)
             outs.append(y.clone())
     finally:
-        call("avt_set_stem_kernel", 0)
+        call("avt_set_stem_kernel", 1)
     assert (outs[0].float() - outs[1].float()).abs().gt(0).float().mean().item() < 0.05
     assert torch.equal(xn[..., :cin].float().cpu(), x.to(torch.bfloat16).permute(0, 2, 3, 1).float())
     dy = _rand_act(N, Pq, Qq, K, 4)
-    dw = torch.zeros(K, R, R, cin, device=DEV)
-    wgrad(xn, dy.to(DEV), dw, N, H, W, cp, cin, K, R, st, pad)
     ref_dw = torch.nn.grad.conv2d_weight(xb, (K, cin, R, R), dy.double().permute(0, 3, 1, 2), stride=st, padding=pad)
-    torch.cuda.synchronize()
-    assert rel_err(dw.permute(0, 3, 1, 2), ref_dw) < 2e-4
+    init = torch.randn(K, R, R, cin, generator=g).to(DEV)  # wgrad accumulates into dw
+    dws = []
+    try:
+        # the per-wave stem wgrad kernel (twice: deterministic), the generic kernel, and the generic
+        # kernel's atomics path (no workspace)
+        for stem_wgrad, slab in ((1, True), (1, True), (0, True), (1, False)):
+            call("avt_set_stem_wgrad", stem_wgrad)
+            dw = init.clone()
+            wgrad(xn, dy.to(DEV), dw, N, H, W, cp, cin, K, R, st, pad, slab=slab)
+            torch.cuda.synchronize()
+            assert rel_err((dw - init).permute(0, 3, 1, 2), ref_dw) < 2e-4, (stem_wgrad, slab)
+            dws.append(dw)
+    finally:
+        call("avt_set_stem_wgrad", 1)
+    assert torch.equal(dws[0], dws[1])
 
 
 @pytest.mark.parametrize("case", CONV_CASES)

@@ -1,6 +1,8 @@
 """Microbenchmark of the 7x7/s2 stem forward kernels at the B=128 trunk shapes: the persistent
 LDS-patch kernel (avt_set_stem_kernel(1)) vs the generic gather kernel (0).  Prints us per launch,
-TFLOP/s of the real (unpadded) FLOPs and the output-store GB/s (the bound: 205 / 317 MB)."""
+TFLOP/s of the real (unpadded) FLOPs and the output-store GB/s (the bound: 205 / 317 MB); then the
+stem wgrads: the per-wave LDS-patch kernel (avt_set_stem_wgrad(1)) vs the generic one, with the
+GB/s of the bytes they must read (input + dy)."""
 import argparse
 import ctypes
 import os
@@ -60,7 +62,22 @@ def main():
                                      S()))
             line += (f" | kernel {kern}: {ms * 1e3:7.1f} us {flops / ms / 1e9:6.0f} TFLOP/s "
                      f"store {out_bytes / ms / 1e6:6.0f} GB/s")
-        call("avt_set_stem_kernel", 0)
+        call("avt_set_stem_kernel", 1)
+        print(line, flush=True)
+        # wgrad: the per-wave stem kernel (+ its slab reduce) vs the generic gather kernel
+        dy = torch.randn(N, OH, OW, K, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(K, R, R, cin, device=dev)
+        in_bytes = 2.0 * N * H * W * cp + 2.0 * N * OH * OW * K
+        line = f"{name:7s} wgrad"
+        for kern in (1, 0):
+            call("avt_set_stem_wgrad", kern)
+            wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, cp, cin, K, R, R, 2, 3))
+            ws = torch.empty(max(wsb, 1), device=dev, dtype=torch.uint8)
+            ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, cp, cin, K, R, R, 2, 3, P(ws),
+                                     wsb, S()))
+            line += (f" | kernel {kern}: {ms * 1e3:7.1f} us {flops / ms / 1e9:6.0f} TFLOP/s "
+                     f"read {in_bytes / ms / 1e6:6.0f} GB/s")
+        call("avt_set_stem_wgrad", 1)
         print(line, flush=True)
 
 
