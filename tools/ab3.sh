@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B/C of bench variants in one GPU session: "<label>:<env assignments>" arguments, alternating, one
-# JSON summary line each.  usage: bash tools/ab3.sh rounds "base:" "s16:AVT_LIB_PATH=..." ...
+# JSON summary line each (extra bench.py flags from $BENCH_ARGS).  usage: bash tools/ab3.sh rounds "base:" "s16:AVT_LIB_PATH=..." ...
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 mkdir -p gpurun_out
@@ -8,7 +8,7 @@ N=$1; shift
 for i in $(seq 1 $N); do
   for spec in "$@"; do
     label=${spec%%:*}; envs=${spec#*:}
-    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/ab3.log 2>&1 || { tail -5 gpurun_out/ab3.log; exit 1; }
+    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/ab3.log 2>&1 || { tail -5 gpurun_out/ab3.log; exit 1; }
     python - "$label" <<'PY'
 import json, sys
 r = json.loads(open("gpurun_out/ab3.log").read().strip().splitlines()[-1])
