@@ -31,6 +31,13 @@ class DgradBnEpi(ctypes.Structure):
                 ("acc2", ctypes.c_void_p), ("skip_class00", ctypes.c_int)]
 
 
+class BnBwdTarget(ctypes.Structure):
+    """avt_bn_bwd_target (include/avt.h): one BatchNorm fed by the masked gradient of avt_bn_bwd_mask."""
+    _fields_ = [("xc", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+                ("gamma", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("gc", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
@@ -52,6 +59,9 @@ SIGNATURES = {
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad_bn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(DgradBnEpi), _P]),
     "avt_bn_bwd_premasked": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_conv2d_dgrad_mask": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_bn_bwd_mask": (_I, [_P, _P, ctypes.POINTER(BnBwdTarget), ctypes.POINTER(BnBwdTarget), _L, _I, _P]),
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),
     "avt_bn_finalize": (_I, [_P, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),

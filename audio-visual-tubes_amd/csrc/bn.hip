@@ -83,12 +83,27 @@ __device__ __forceinline__ int chan_block(long long i, int cv) {
   return POW2 ? (int)((unsigned)i & (unsigned)(cv - 1)) : (int)(i % cv);
 }
 
+// Bit e of the result: bf16 element e of v is > 0 (positive and non-zero as int16) -- the ReLU
+// backward's `result > 0` evaluated on the stored output.
+__device__ __forceinline__ unsigned pos_bits8(const u32x4& v) {
+  const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+  unsigned b = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    b |= ((short)(u[e] & 0xffff) > 0 ? 1u : 0u) << (2 * e);
+    b |= ((short)(u[e] >> 16) > 0 ? 1u : 0u) << (2 * e + 1);
+  }
+  return b;
+}
+
+// mk (optional, with relu): the ReLU mask of out as bits, one byte per 8 channels ([rows][C/8] u8):
+// the backward reads 1/16 of the bytes of out for it.
 template <bool POW2>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        const bf16_t* __restrict__ res, const float* __restrict__ rscale,
                                                        const float* __restrict__ rshift, bf16_t* __restrict__ out,
-                                                       long long nvec, int C, int relu) {
+                                                       unsigned char* __restrict__ mk, long long nvec, int C, int relu) {
   const int cv = C / 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nvec; i += (long long)gridDim.x * blockDim.x) {
     const int c0 = chan_block<POW2>(i, cv) * 8;
@@ -111,7 +126,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
     }
-    reinterpret_cast<u32x4*>(out)[i] = pack8(f);
+    const u32x4 o = pack8(f);
+    reinterpret_cast<u32x4*>(out)[i] = o;
+    if (mk) mk[i] = (unsigned char)pos_bits8(o);
   }
 }
 
@@ -219,10 +236,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 }
 
 // dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
-                                                              float* dgamma, float* dbeta, float* k1, float* k2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, double inv_rows,
+                                                    float* dgamma, float* dbeta, float* k1, float* k2) {
   double a = 0.0, b = 0.0;
 #pragma unroll
   for (int s = 0; s < AVT_BN_SLOTS; ++s) {
@@ -236,6 +251,24 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict
   if (dgamma) dgamma[c] += (float)b;
   k1[c] = (float)(a * inv_rows);
   k2[c] = (float)(b * inv_rows);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
+                                                              float* dgamma, float* dbeta, float* k1, float* k2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) bn_bwd_finalize_one(acc, C, c, inv_rows, dgamma, dbeta, k1, k2);
+}
+
+// both BNs of a first block in one launch: threads [0, C) the first, [C, 2C) the second
+__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(double* __restrict__ acc, double* __restrict__ acc2,
+                                                               int C, double inv_rows, float* dgamma, float* dbeta,
+                                                               float* k1, float* k2, float* dgamma2, float* dbeta2,
+                                                               float* k1b, float* k2b) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C)
+    bn_bwd_finalize_one(acc, C, c, inv_rows, dgamma, dbeta, k1, k2);
+  else if (c < 2 * C)
+    bn_bwd_finalize_one(acc2, C, c - C, inv_rows, dgamma2, dbeta2, k1b, k2b);
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
@@ -263,6 +296,160 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restr
     }
     reinterpret_cast<u32x4*>(gc)[i] = pack8(o);
     if (gmask_out) reinterpret_cast<u32x4*>(gmask_out)[i] = pack8(gg);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Block-output BN backward from the ReLU mask bits (avt_bn_apply_mask): g' = g * bit, and -- for a
+// first block -- bn2 and downsample.1 in one pass over (g, mask, xc, xc2): they share g' (the ReLU
+// sits after their sum, base_models.py:64-67), so g and the mask are read once for both.
+struct MaskBwdArgs {
+  const bf16_t* g;
+  const unsigned char* mk;  // [rows][C/8] mask bits
+  const bf16_t* xc;
+  const float* mean;
+  const float* invstd;
+  double* acc;              // [SLOTS][C][2]: (sum g', sum g' * xhat)
+  const bf16_t* xc2;        // TWO: the second BN's pre-activation / statistics / accumulator
+  const float* mean2;
+  const float* invstd2;
+  double* acc2;
+  long long rows;
+  int C, rows_per_block;
+};
+
+__device__ __forceinline__ void mask8(float* gg, unsigned bits) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) gg[e] = (bits >> e) & 1u ? gg[e] : 0.f;
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_mask_reduce_kernel(MaskBwdArgs a) {
+  constexpr int NS = TWO ? 3 : 2;
+  __shared__ float red[2048 * NS];  // [256/(C/8)][C][NS]
+  const int C = a.C, cv = C / 8;
+  const int chunk = threadIdx.x % cv, r0 = threadIdx.x / cv, rstep = 256 / cv;
+  const int c0 = chunk * 8;
+  float mu[8], is[8], mu2[8], is2[8], s1[8], s2[8], s3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = a.mean[c0 + e];
+    is[e] = a.invstd[c0 + e];
+    if (TWO) {
+      mu2[e] = a.mean2[c0 + e];
+      is2[e] = a.invstd2[c0 + e];
+    }
+    s1[e] = s2[e] = s3[e] = 0.f;
+  }
+  const long long rbeg = (long long)blockIdx.x * a.rows_per_block;
+  const long long rend = min(a.rows, rbeg + a.rows_per_block);
+  auto body = [&](const u32x4& gq, unsigned bits, const u32x4& xq, const u32x4& x2q) {
+    float gg[8], xx[8];
+    unpack8(gq, gg);
+    unpack8(xq, xx);
+    mask8(gg, bits);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += gg[e];
+      s2[e] += gg[e] * (xx[e] - mu[e]) * is[e];
+    }
+    if (TWO) {
+      float x2[8];
+      unpack8(x2q, x2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s3[e] += gg[e] * (x2[e] - mu2[e]) * is2[e];
+    }
+  };
+  long long r = rbeg + r0;
+  constexpr int U = 4;  // rows in flight per thread (HBM-bound: bytes in flight per CU)
+  for (; r + (U - 1) * rstep < rend; r += U * rstep) {
+    u32x4 gq[U], xq[U], x2q[U];
+    unsigned bq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t o = (size_t)(r + u * rstep) * cv + chunk;
+      gq[u] = reinterpret_cast<const u32x4*>(a.g)[o];
+      xq[u] = reinterpret_cast<const u32x4*>(a.xc)[o];
+      if (TWO) x2q[u] = reinterpret_cast<const u32x4*>(a.xc2)[o];
+      bq[u] = a.mk[o];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(gq[u], bq[u], xq[u], TWO ? x2q[u] : xq[u]);
+  }
+  for (; r < a.rows && r < rend; r += rstep) {
+    const size_t o = (size_t)r * cv + chunk;
+    const u32x4 gq = reinterpret_cast<const u32x4*>(a.g)[o];
+    const u32x4 xq = reinterpret_cast<const u32x4*>(a.xc)[o];
+    body(gq, a.mk[o], xq, TWO ? reinterpret_cast<const u32x4*>(a.xc2)[o] : xq);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(r0 * C + c0 + e) * NS] = s1[e];
+    red[(r0 * C + c0 + e) * NS + 1] = s2[e];
+    if (TWO) red[(r0 * C + c0 + e) * NS + 2] = s3[e];
+  }
+  __syncthreads();
+  const size_t slot = (size_t)(blockIdx.x % AVT_BN_SLOTS) * C * 2;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float x = 0.f, y = 0.f, z = 0.f;
+    for (int k = 0; k < rstep; ++k) {
+      x += red[(k * C + c) * NS];
+      y += red[(k * C + c) * NS + 1];
+      if (TWO) z += red[(k * C + c) * NS + 2];
+    }
+    atomicAdd(a.acc + slot + 2 * c, (double)x);
+    atomicAdd(a.acc + slot + 2 * c + 1, (double)y);
+    if (TWO) {
+      atomicAdd(a.acc2 + slot + 2 * c, (double)x);
+      atomicAdd(a.acc2 + slot + 2 * c + 1, (double)z);
+    }
+  }
+}
+
+// gc = gamma*invstd*(g' - k1 - xhat*k2) (and gc2 for the second BN) from the finalized k1/k2
+struct MaskApplyArgs {
+  const bf16_t* g;
+  const unsigned char* mk;
+  const bf16_t* xc;
+  const float *mean, *invstd, *gamma, *k1, *k2;
+  bf16_t* gc;
+  const bf16_t* xc2;
+  const float *mean2, *invstd2, *gamma2, *k1b, *k2b;
+  bf16_t* gc2;
+  long long nvec;
+  int C;
+};
+
+template <bool TWO>
+__global__ __launch_bounds__(256) void bn_bwd_mask_apply_kernel(MaskApplyArgs a) {
+  const int cv = a.C / 8;  // a power of two dividing 256 (checked by the host)
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < a.nvec;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((unsigned)i & (unsigned)(cv - 1)) * 8;
+    float gg[8], xx[8], o[8];
+    unpack8(reinterpret_cast<const u32x4*>(a.g)[i], gg);
+    unpack8(reinterpret_cast<const u32x4*>(a.xc)[i], xx);
+    const unsigned bits = a.mk[i];
+    u32x4 x2q;
+    if (TWO) x2q = reinterpret_cast<const u32x4*>(a.xc2)[i];
+    mask8(gg, bits);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float xh = (xx[e] - a.mean[c]) * a.invstd[c];
+      o[e] = a.gamma[c] * a.invstd[c] * (gg[e] - a.k1[c] - xh * a.k2[c]);
+    }
+    reinterpret_cast<u32x4*>(a.gc)[i] = pack8(o);
+    if (TWO) {
+      unpack8(x2q, xx);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        const float xh = (xx[e] - a.mean2[c]) * a.invstd2[c];
+        o[e] = a.gamma2[c] * a.invstd2[c] * (gg[e] - a.k1b[c] - xh * a.k2b[c]);
+      }
+      reinterpret_cast<u32x4*>(a.gc2)[i] = pack8(o);
+    }
   }
 }
 
@@ -494,11 +681,96 @@ extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shif
   const int grid = ew_grid(nvec);
   if (256 % (C / 8) == 0)
     hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, scale,
-                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
+                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nullptr, nvec, C, relu);
   else
     hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, scale,
-                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nvec, C, relu);
+                       shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, nullptr, nvec, C, relu);
   return check_launch("bn_apply");
+}
+
+extern "C" int avt_bn_apply_mask(const void* x, const float* scale, const float* shift, const void* residual,
+                                 const float* rscale, const float* rshift, void* out, void* mask, long long rows,
+                                 int C, void* stream) {
+  AVT_REQUIRE(x && scale && shift && out && mask, "bn_apply_mask: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_apply_mask: C=%d unsupported", C);
+  AVT_REQUIRE((rscale == nullptr) == (rshift == nullptr), "bn_apply_mask: rscale/rshift must be both set or both null");
+  const long long nvec = rows * C / 8;
+  if (nvec == 0) return AVT_OK;
+  hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     scale, shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, (unsigned char*)mask, nvec, C,
+                     1);
+  return check_launch("bn_apply_mask");
+}
+
+extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd_target* t1,
+                               const avt_bn_bwd_target* t2, long long rows, int C, void* stream) {
+  AVT_REQUIRE(g && mask && t1, "bn_bwd_mask: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "bn_bwd_mask: C=%d unsupported", C);
+  AVT_REQUIRE(rows > 0, "bn_bwd_mask: empty input");
+  const avt_bn_bwd_target* ts[2] = {t1, t2};
+  for (int k = 0; k < (t2 ? 2 : 1); ++k) {
+    const avt_bn_bwd_target* t = ts[k];
+    AVT_REQUIRE(t->xc && t->mean && t->invstd && t->gamma && t->gc && t->workspace, "bn_bwd_mask: null target pointer");
+    AVT_REQUIRE(((uintptr_t)t->workspace & 7) == 0, "bn_bwd_mask: workspace must be 8-byte aligned");
+  }
+  hipStream_t st = (hipStream_t)stream;
+  double* acc = (double*)t1->workspace;
+  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  double* acc2 = t2 ? (double*)t2->workspace : nullptr;
+  float* k1b = t2 ? (float*)(acc2 + (size_t)AVT_BN_SLOTS * C * 2) : nullptr;
+  MaskBwdArgs a{};
+  a.g = (const bf16_t*)g;
+  a.mk = (const unsigned char*)mask;
+  a.xc = (const bf16_t*)t1->xc;
+  a.mean = t1->mean;
+  a.invstd = t1->invstd;
+  a.acc = acc;
+  if (t2) {
+    a.xc2 = (const bf16_t*)t2->xc;
+    a.mean2 = t2->mean;
+    a.invstd2 = t2->invstd;
+    a.acc2 = acc2;
+  }
+  a.rows = rows;
+  a.C = C;
+  long long rpb = (rows + 511) / 512;  // ~2 blocks per CU of rows, as bn_bwd_reduce_launch
+  const int rstep = 256 / (C / 8);
+  rpb = ((rpb + rstep - 1) / rstep) * rstep;
+  if (rpb < rstep) rpb = rstep;
+  a.rows_per_block = (int)rpb;
+  const int nblk = (int)((rows + rpb - 1) / rpb);
+  const double inv_rows = 1.0 / (double)rows;
+  MaskApplyArgs p{};
+  p.g = a.g;
+  p.mk = a.mk;
+  p.xc = a.xc;
+  p.mean = t1->mean;
+  p.invstd = t1->invstd;
+  p.gamma = t1->gamma;
+  p.k1 = k1;
+  p.k2 = k1 + C;
+  p.gc = (bf16_t*)t1->gc;
+  p.nvec = rows * C / 8;
+  p.C = C;
+  if (t2) {
+    hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, acc, acc2, C, inv_rows,
+                       t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
+    p.xc2 = (const bf16_t*)t2->xc;
+    p.mean2 = t2->mean;
+    p.invstd2 = t2->invstd;
+    p.gamma2 = t2->gamma;
+    p.k1b = k1b;
+    p.k2b = k1b + C;
+    p.gc2 = (bf16_t*)t2->gc;
+    hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
+                       t1->dbeta, k1, k1 + C);
+    hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
+  }
+  return check_launch("bn_bwd_mask");
 }
 
 // workspace: AVT_BN_SLOTS*C*2 doubles (must be zero on entry; left zero on exit) + 2*C floats

@@ -9,6 +9,15 @@
 // Included by conv_gemm.hip inside namespace avt.
 #pragma once
 
+// zero the bf16 elements of v whose bit in `bits` is clear
+__device__ __forceinline__ u32x4 epi_mask8(u32x4 v, unsigned bits) {
+  unsigned* u = reinterpret_cast<unsigned*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    u[e] &= ((bits >> (2 * e)) & 1u ? 0x0000ffffu : 0u) | ((bits >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+  return v;
+}
+
 __device__ __forceinline__ void epi_unpack8(const u32x4& v, float* f) {
   const unsigned* u = reinterpret_cast<const unsigned*>(&v);
 #pragma unroll
@@ -51,7 +60,10 @@ __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t
       const int r = (tid + (it0 + u) * NT) / OCPR;
       ok[u] = r < rows_valid;
       off[u] = ok[u] ? orow(r) * (size_t)p.Ng + c0 : 0;
-      if (ok[u] && has_add) aa[u] = *reinterpret_cast<const u32x4*>(p.add + off[u]);
+      if (ok[u] && has_add) {
+        aa[u] = *reinterpret_cast<const u32x4*>(p.add + off[u]);
+        if (p.amask) aa[u] = epi_mask8(aa[u], p.amask[off[u] >> 3]);
+      }
       if (ok[u] && bnb) {
         xx[u] = *reinterpret_cast<const u32x4*>(p.bx + off[u]);
         if (has_y) yy[u] = *reinterpret_cast<const u32x4*>(p.by + off[u]);
@@ -166,7 +178,8 @@ __device__ __forceinline__ void epi_store(const GemmNTParams& p, const bf16_t* C
       u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * ct_ld + cc * 8);
       const size_t off = orow(r) * (size_t)p.Ng + n0 + cc * 8;
       if (p.add != nullptr) {
-        const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+        u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+        if (p.amask != nullptr) a = epi_mask8(a, p.amask[off >> 3]);
         unsigned* vv = reinterpret_cast<unsigned*>(&v);
         const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
 #pragma unroll

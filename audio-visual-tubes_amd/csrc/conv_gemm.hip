@@ -48,6 +48,8 @@ struct GemmNTParams {
   double* bacc2;
   int bskip00;         // host side: a stride-2 dgrad's class-(0,0) launch stores plain g (another
                        // kernel -- the downsample dgrad -- adds to those pixels and applies the epilogue)
+  const unsigned char* amask;  // optional [M][Ng/8] bits: `add` enters masked, add * bit (an identity
+                               // block's residual gradient g * [out > 0], from avt_bn_apply_mask's bits)
 };
 
 __device__ __forceinline__ int swz64(int row, int chunk) {  // byte offset in a [rows][32 bf16] tile
@@ -277,9 +279,15 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
     u32x4 v = *reinterpret_cast<const u32x4*>(Ct + r * CT_LD + cc * 8);
     const size_t off = (size_t)(m0 + r) * p.Ng + n0 + cc * 8;
     if (p.add != nullptr) {
-      const u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
+      u32x4 a = *reinterpret_cast<const u32x4*>(p.add + off);
       unsigned* vv = reinterpret_cast<unsigned*>(&v);
-      const unsigned* aa = reinterpret_cast<const unsigned*>(&a);
+      unsigned* aa = reinterpret_cast<unsigned*>(&a);
+      if (p.amask != nullptr) {
+        const unsigned bits = p.amask[off >> 3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          aa[e] &= ((bits >> (2 * e)) & 1u ? 0x0000ffffu : 0u) | ((bits >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float lo = bf2f(vv[e] & 0xffff) + bf2f(aa[e] & 0xffff);
@@ -855,9 +863,9 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   return check_launch("conv2d_fwd");
 }
 
-extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W,
-                                   int C, int K, int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi,
-                                   void* stream) {
+static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
+                             int H, int W, int C, int K, int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi,
+                             void* stream) {
   AVT_REQUIRE(dy && wt && dx, "conv2d_dgrad: null pointer");
   AVT_REQUIRE(epi == nullptr || (epi->xc && epi->stats && epi->acc), "conv2d_dgrad: epilogue needs xc, stats, acc");
   AVT_REQUIRE(epi == nullptr || epi->xc2 == nullptr || (epi->stats2 && epi->acc2),
@@ -871,6 +879,7 @@ extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, con
   p.wmat = (const bf16_t*)wt;
   p.out = (bf16_t*)dx;
   p.add = (const bf16_t*)add;
+  p.amask = (const unsigned char*)add_mask;
   p.stats = nullptr;
   p.IH = conv_out(H, R, stride, pad);
   p.IW = conv_out(W, S, stride, pad);
@@ -902,9 +911,23 @@ extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, con
   return check_launch("conv2d_dgrad");
 }
 
+extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W,
+                                   int C, int K, int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi,
+                                   void* stream) {
+  return conv2d_dgrad_impl(dy, wt, dx, add, nullptr, N, H, W, C, K, R, S, stride, pad, epi, stream);
+}
+
 extern "C" int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C,
                                 int K, int R, int S, int stride, int pad, void* stream) {
-  return avt_conv2d_dgrad_bn(dy, wt, dx, add, N, H, W, C, K, R, S, stride, pad, nullptr, stream);
+  return conv2d_dgrad_impl(dy, wt, dx, add, nullptr, N, H, W, C, K, R, S, stride, pad, nullptr, stream);
+}
+
+extern "C" int avt_conv2d_dgrad_mask(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask,
+                                     int N, int H, int W, int C, int K, int R, int S, int stride, int pad,
+                                     void* stream) {
+  AVT_REQUIRE(add && add_mask, "conv2d_dgrad_mask: add and add_mask are required");
+  AVT_REQUIRE(add != dx, "conv2d_dgrad_mask: add must not alias dx");
+  return conv2d_dgrad_impl(dy, wt, dx, add, add_mask, N, H, W, C, K, R, S, stride, pad, nullptr, stream);
 }
 
 // Conv3d forward (the R3D-18 video trunk, models/resnet3D.py:14-28 conv3x3x3 / conv1x1x1, called

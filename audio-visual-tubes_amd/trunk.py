@@ -15,7 +15,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ._lib import DgradBnEpi, call, query
+from ._lib import BnBwdTarget, DgradBnEpi, call, query
 
 STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
 # 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
@@ -236,15 +236,22 @@ class Trunk:
                  stream_ptr())
             c2, s2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training)
             out = torch.empty_like(c2)
+            # training: the output's ReLU mask as bits ([rows][C/8] u8) for the backward, which then never
+            # re-reads `out` (1/16 of its bytes)
+            om = torch.empty(c2.numel() // 8, device=x.device, dtype=torch.uint8) if training else None
             if blk["down"] is not None:
                 cd, sd, _, _ = self._conv_bn(cur, N, Hc, Wc, blk["down"], blk["bnd"], store, training)
-                call("avt_bn_apply", P(c2), P(s2[0]), P(s2[1]), P(cd), P(sd[0]), P(sd[1]), P(out), N * Ho * Wo,
-                     c2.shape[-1], 1, stream_ptr())
+                res = (P(cd), P(sd[0]), P(sd[1]))
                 t.update(cd=cd, sd=sd)
             else:
-                call("avt_bn_apply", P(c2), P(s2[0]), P(s2[1]), P(cur), None, None, P(out), N * Ho * Wo, c2.shape[-1],
-                     1, stream_ptr())
-            t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, Ho=Ho, Wo=Wo)
+                res = (P(cur), None, None)
+            if training:
+                call("avt_bn_apply_mask", P(c2), P(s2[0]), P(s2[1]), *res, P(out), P(om), N * Ho * Wo, c2.shape[-1],
+                     stream_ptr())
+            else:
+                call("avt_bn_apply", P(c2), P(s2[0]), P(s2[1]), *res, P(out), N * Ho * Wo, c2.shape[-1], 1,
+                     stream_ptr())
+            t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, om=om, Ho=Ho, Wo=Wo)
             tape["blocks"].append(t)
             cur, Hc, Wc = out, Ho, Wo
         if not training:
@@ -260,6 +267,28 @@ class Trunk:
              P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc), P(gmask_out), P(ws),
              rows, bn.c, stream_ptr())
         return gc
+
+    def _target(self, xc, stats, bn: BNSpec, store: Store) -> BnBwdTarget:
+        t = BnBwdTarget()
+        gc = torch.empty_like(xc)
+        t.xc, t.mean, t.invstd = xc.data_ptr(), stats[2].data_ptr(), stats[3].data_ptr()
+        t.gamma = store.param(bn.prefix + ".weight").data_ptr()
+        dg, db = store.grad(bn.prefix + ".weight"), store.grad(bn.prefix + ".bias")
+        t.dgamma = dg.data_ptr() if dg is not None else None
+        t.dbeta = db.data_ptr() if db is not None else None
+        t.gc = gc.data_ptr()
+        t.workspace = store.stat_acc(bn, "bwd").data_ptr()
+        t.keep = gc  # the output tensor (ctypes.Structure keeps no reference)
+        return t
+
+    def _bn_bwd_mask(self, g, mask, xc, stats, bn: BNSpec, store: Store, xc2=None, stats2=None, bn2=None):
+        """Block-output BN backward(s) from the ReLU mask bits: bn2 alone, or bn2 + downsample.1 in one
+        pass (avt_bn_bwd_mask).  Returns the gradient(s) of the pre-BN activation(s)."""
+        t1 = self._target(xc, stats, bn, store)
+        t2 = self._target(xc2, stats2, bn2, store) if bn2 is not None else None
+        call("avt_bn_bwd_mask", P(g), P(mask), ctypes.byref(t1), ctypes.byref(t2) if t2 is not None else None,
+             xc.numel() // bn.c, bn.c, stream_ptr())
+        return t1.keep, (t2.keep if t2 is not None else None)
 
     def _bn_relu_bwd(self, g, xc, stats, bn: BNSpec, store: Store):
         """bn -> relu backward with the mask recomputed from (xc, scale, shift) (BasicBlock.bn1)."""
@@ -282,7 +311,7 @@ class Trunk:
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
 
-    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False, epi=None):
+    def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False, epi=None, add_mask=None):
         """inplace: accumulate into `add` (dx = add + dgrad); a strided 1x1 conv then only touches the
         pixels its taps reach (the other parity classes of avt_conv2d_dgrad are skipped).
         epi: DgradBnEpi -- the backward reductions of the BN+ReLU that produced dx's positions fused into
@@ -290,7 +319,11 @@ class Trunk:
         _, wt = store.packed(spec)
         gx = add if inplace else torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
         ev = ConvProfiler.begin()
-        if epi is None:
+        if add_mask is not None:  # dx = dgrad + add * mask bits
+            assert epi is None
+            call("avt_conv2d_dgrad_mask", P(gy), P(wt), P(gx), P(add), P(add_mask), N, H, W, spec.cin, spec.cout,
+                 spec.k, spec.k, spec.stride, spec.pad, stream_ptr())
+        elif epi is None:
             call("avt_conv2d_dgrad", P(gy), P(wt), P(gx), P(add), N, H, W, spec.cin, spec.cout, spec.k, spec.k,
                  spec.stride, spec.pad, stream_ptr())
         else:
@@ -344,10 +377,18 @@ class Trunk:
                 gres = g
                 g_c2 = self._bn_bwd_premasked(g, t["c2"], t["s2"], blk["bn2"], store)
                 g_cd = None if identity else self._bn_bwd_premasked(g, t["cd"], t["sd"], blk["bnd"], store)
-            else:
-                gres = torch.empty_like(t["c2"]) if identity else None
-                g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gres)
-                g_cd = None if identity else self._bn_bwd(g, t["out"], t["cd"], t["sd"], blk["bnd"], store)
+            else:  # g' = g * [out > 0] from the forward's mask bits; an identity block's residual gradient
+                # enters the conv1 dgrad below as (g, mask) instead of a stored g'
+                gres = None
+                if identity and FUSE_BN_BWD and bi > 0:  # conv1's dgrad below carries a BN epilogue: store g'
+                    gres = torch.empty_like(t["c2"])
+                    g_c2 = self._bn_bwd(g, t["out"], t["c2"], t["s2"], blk["bn2"], store, gmask_out=gres)
+                    g_cd = None
+                elif identity:
+                    g_c2, g_cd = self._bn_bwd_mask(g, t["om"], t["c2"], t["s2"], blk["bn2"], store)
+                else:
+                    g_c2, g_cd = self._bn_bwd_mask(g, t["om"], t["c2"], t["s2"], blk["bn2"], store,
+                                                   t["cd"], t["sd"], blk["bnd"])
             self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
             if FUSE_BN_BWD:  # conv2 dgrad with bn1's backward (ReLU mask from its pre-activation) in the epilogue
                 g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store,
@@ -367,7 +408,9 @@ class Trunk:
                                               bn2=pb["bnd"] if has_d else None, xc2=pt["cd"] if has_d else None,
                                               stats2=pt["sd"] if has_d else None, skip00=skip00)
                 epi = mk(False)
-            if identity:
+            if identity and gres is None:
+                g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=g, epi=epi, add_mask=t["om"])
+            elif identity:
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=gres, epi=epi)
             else:
                 # the downsample dgrad (in place) finishes every pixel it reaches: the epilogue goes there;

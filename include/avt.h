@@ -105,6 +105,11 @@ int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, in
 /* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
 int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
                      int R, int S, int stride, int pad, void* stream);
+/* dx = dgrad(dy, wt) + add * mask: an identity BasicBlock's input gradient (base_models.py:64-67), the
+ * residual branch entering as g * [out > 0] with the bits of avt_bn_apply_mask ([N*H*W][C/8] u8) --
+ * the masked copy of g is never stored.  add must not alias dx. */
+int avt_conv2d_dgrad_mask(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
+                          int H, int W, int C, int K, int R, int S, int stride, int pad, void* stream);
 /* avt_conv2d_dgrad with the backward of the BatchNorm (+ReLU) that produced dx's positions fused into
  * its store epilogue (BasicBlock.forward, base_models.py:46-49, 58-67): the result g (after `add`) is
  * masked, g' = g * [y > 0] (y given: the block output) or g * [fma(xc, scale, shift) > 0] (y NULL:
@@ -161,6 +166,10 @@ int avt_bn_finalize_rep(double* acc, long long rows, long long rep, int C, const
 /* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
 int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                  const float* rshift, void* out, long long rows, int C, int relu, void* stream);
+/* avt_bn_apply with relu, also writing the ReLU mask of out as bits: mask [rows][C/8] u8, bit e of byte
+ * j = out[.][8j+e] > 0 (the stored bf16 value) -- what the backward's relu mask reads instead of out */
+int avt_bn_apply_mask(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
+                      const float* rshift, void* out, void* mask, long long rows, int C, void* stream);
 /* bytes of bn_bwd workspace: its first avt_bn_slots()*C*2 doubles must be zero on entry (left zero) */
 size_t avt_bn_bwd_workspace(long long rows, int C);
 /* g' = g*[y>0] (y may be NULL: no mask); dgamma += sum g'*xhat; dbeta += sum g';
@@ -168,6 +177,22 @@ size_t avt_bn_bwd_workspace(long long rows, int C);
 int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
                const float* gamma, float* dgamma, float* dbeta, void* gc, void* gmask_out, void* workspace,
                long long rows, int C, void* stream);
+/* one BatchNorm fed by g' (see avt_bn_bwd_mask) */
+typedef struct {
+  const void* xc;         /* [rows][C] bf16 pre-BN activations */
+  const float* mean;      /* [C] batch mean / invstd (avt_bn_finalize save_mean / save_invstd) */
+  const float* invstd;
+  const float* gamma;
+  float* dgamma;          /* [C] accumulated (+=), may be NULL */
+  float* dbeta;
+  void* gc;               /* [rows][C] bf16 output: gradient of xc */
+  void* workspace;        /* avt_bn_bwd_workspace(rows, C) bytes, accumulator zero on entry (left zero) */
+} avt_bn_bwd_target;
+/* BasicBlock output backward (base_models.py:64-67): g' = g * mask (bits of avt_bn_apply_mask), then the
+ * BN backward of t1 and -- if t2 != NULL -- of t2 (a first block's bn2 and downsample.1, which share g'),
+ * reading g and the mask once for both */
+int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd_target* t1, const avt_bn_bwd_target* t2,
+                    long long rows, int C, void* stream);
 /* avt_bn_bwd for a g' that is already masked and whose reductions a dgrad epilogue already added
  * into the workspace (avt_conv2d_dgrad_bn): finalize + apply only */
 int avt_bn_bwd_premasked(const void* gm, const void* xc, const float* mean, const float* invstd, const float* gamma,

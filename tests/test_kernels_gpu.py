@@ -292,6 +292,16 @@ def test_conv_dgrad(case, tiles):
     call("avt_conv2d_dgrad", P(D(dy)), P(wt), P(dx2), P(D(add)), N, H, W, C, K, R, R, st, pad, S())
     torch.cuda.synchronize()
     assert rel_err(dx2, ref + add.double()) < 8e-3
+    # masked accumulate (identity block: dx = dgrad + g * [out > 0] from avt_bn_apply_mask's bits): bitwise
+    # equal to the plain accumulate of the pre-masked add
+    bits = torch.randint(0, 256, (N * H * W * C // 8,), generator=torch.Generator().manual_seed(8), dtype=torch.uint8)
+    keep = ((bits.long().unsqueeze(1) >> torch.arange(8)) & 1).bool().reshape(N, H, W, C)
+    addm = torch.where(keep, add, torch.zeros_like(add))
+    dx3, dx4 = torch.empty_like(dx), torch.empty_like(dx)
+    call("avt_conv2d_dgrad", P(D(dy)), P(wt), P(dx3), P(D(addm)), N, H, W, C, K, R, R, st, pad, S())
+    call("avt_conv2d_dgrad_mask", P(D(dy)), P(wt), P(dx4), P(D(add)), P(D(bits)), N, H, W, C, K, R, R, st, pad, S())
+    torch.cuda.synchronize()
+    assert torch.equal(dx3, dx4)
 
 
 def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
@@ -412,6 +422,73 @@ def test_bn_backward(shape, masked):
     assert rel_err(gc, cn.grad.permute(0, 2, 3, 1)) < 2e-2
     assert rel_err(dgamma, gm.grad) < 1e-2
     assert rel_err(dbeta, bt.grad) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128), (2, 17, 19, 256)])
+@pytest.mark.parametrize("two", [False, True])
+def test_bn_mask_bits_fwd_bwd(shape, two):
+    """avt_bn_apply_mask = avt_bn_apply + the ReLU bits of out; avt_bn_bwd_mask (one BN, or bn2 +
+    downsample.1 sharing g') = avt_bn_bwd fed y = out, per BN; and the fp64 autograd of the block's
+    relu(bn2(c2) + bnd(cd))."""
+    N, H, W, C = shape
+    rows = N * H * W
+    c = (_rand_act(N, H, W, C, 31).float() * 1.3 - 0.2).to(torch.bfloat16)
+    cd = (_rand_act(N, H, W, C, 32).float() * 0.9 + 0.1).to(torch.bfloat16)
+    gy = _rand_act(N, H, W, C, 33)
+    g = torch.Generator().manual_seed(34)
+    gam, bet = 1 + 0.02 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    gam2, bet2 = 1 + 0.02 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    st, st2 = _bn_batch_stats(c, gam, bet), _bn_batch_stats(cd, gam2, bet2)
+    cdev, cddev, gydev = D(c), D(cd), D(gy)
+    res = (P(cddev), P(st2[0]), P(st2[1])) if two else (P(cddev), None, None)
+    y = torch.empty_like(cdev)
+    y2 = torch.empty_like(cdev)
+    bits = torch.empty(rows * C // 8, device=DEV, dtype=torch.uint8)
+    call("avt_bn_apply", P(cdev), P(st[0]), P(st[1]), *res, P(y), rows, C, 1, S())
+    call("avt_bn_apply_mask", P(cdev), P(st[0]), P(st[1]), *res, P(y2), P(bits), rows, C, S())
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    pos = (y.float() > 0).reshape(-1, 8).cpu().long()
+    assert torch.equal(bits.cpu().long(), (pos << torch.arange(8)).sum(1))
+    from avt_amd._lib import BnBwdTarget
+
+    def target(xc, s, gamma):
+        t = BnBwdTarget()
+        t.keep = [torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.empty_like(xc),
+                  torch.zeros(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8), D(gamma)]
+        t.xc, t.mean, t.invstd, t.gamma = xc.data_ptr(), s[2].data_ptr(), s[3].data_ptr(), t.keep[4].data_ptr()
+        t.dgamma, t.dbeta, t.gc, t.workspace = [k.data_ptr() for k in t.keep[:4]]
+        return t
+
+    t1 = target(cdev, st, gam)
+    t2 = target(cddev, st2, gam2) if two else None
+    call("avt_bn_bwd_mask", P(gydev), P(bits), ctypes.byref(t1), ctypes.byref(t2) if two else None, rows, C, S())
+    torch.cuda.synchronize()
+    for t, xc, s, gamma in ([(t1, cdev, st, gam)] + ([(t2, cddev, st2, gam2)] if two else [])):
+        assert not t.keep[3][: 16 * C * 2 * 8].any()  # accumulator left zeroed
+        ws = torch.zeros(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
+        dg, db, gc = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.empty_like(xc)
+        call("avt_bn_bwd", P(gydev), P(y), P(xc), P(s[2]), P(s[3]), P(D(gamma)), P(dg), P(db), P(gc), None, P(ws),
+             rows, C, S())
+        torch.cuda.synchronize()
+        # same mask and sums; only the fp64 atomic order may move k1/k2 by an ulp (-> a bf16 ulp of gc)
+        torch.testing.assert_close(t.keep[2].float(), gc.float(), rtol=8e-3, atol=1e-4)
+        torch.testing.assert_close(t.keep[0], dg, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(t.keep[1], db, rtol=1e-5, atol=1e-6)
+    # fp64 autograd of the block output relu(bn2(c) + [bnd(cd) | cd])
+    cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
+    cdn = cd.double().permute(0, 3, 1, 2).requires_grad_(True)
+    gm, bt = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    gm2, bt2 = gam2.double().requires_grad_(True), bet2.double().requires_grad_(True)
+    r = F.batch_norm(cdn, None, None, gm2, bt2, True, 0.1, 1e-5) if two else cdn
+    (F.batch_norm(cn, None, None, gm, bt, True, 0.1, 1e-5) + r).relu().backward(gy.double().permute(0, 3, 1, 2))
+    assert rel_err(t1.keep[2], cn.grad.permute(0, 2, 3, 1)) < 2e-2
+    assert rel_err(t1.keep[0], gm.grad) < 1e-2
+    assert rel_err(t1.keep[1], bt.grad) < 1e-3
+    if two:
+        assert rel_err(t2.keep[2], cdn.grad.permute(0, 2, 3, 1)) < 2e-2
+        assert rel_err(t2.keep[0], gm2.grad) < 1e-2
+        assert rel_err(t2.keep[1], bt2.grad) < 1e-3
 
 
 def _bn_batch_stats(c, gamma, beta):
