@@ -483,6 +483,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
 #include "conv_nt_pipe.h"
 #include "conv_tn_pipe.h"
 #include "conv_halo.h"
+#include "conv_c64.h"
 #include "conv_wgrad_halo.h"
 #include "conv_stem.h"
 #include "conv_stem_wgrad.h"
@@ -536,6 +537,15 @@ static int halo_enabled() {
   }
   return g_halo;
 }
+static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
+static int c64_enabled() {
+  if (g_c64 < 0) {
+    const char* e = getenv("AVT_C64");
+    g_c64 = e ? atoi(e) : 1;
+  }
+  return g_c64;
+}
+
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -551,6 +561,11 @@ using namespace avt;
 
 extern "C" int avt_set_conv_variant(int v) {
   avt::g_conv_variant = v;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_c64(int on) {
+  g_c64 = on ? 1 : 0;
   return AVT_OK;
 }
 
@@ -740,8 +755,55 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st) {
                        p, ha);
 }
 
+// C = K = 64 3x3/s1/p1 Conv2d (the layer-1 convs), image width <= 95, not a BN-epilogue dgrad and not
+// in-place: the persistent resident-weight kernel (conv_c64.h); off with the halo kernels (halo 0: the
+// tap-gather kernel everywhere, as the bitwise-order tests need) or avt_set_c64(0)
+static bool c64_eligible(const GemmNTParams& p) {
+  return c64_enabled() && halo_enabled() && conv_variant() == 1 && p.IC == 64 && p.Ng == 64 && p.Kg == 576 &&
+         p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.IT == 1 && p.OT == 1 && p.IH == p.OH &&
+         p.IW == p.OW && 256 + 2 * p.OW + 2 <= c64::PRMAX && p.bx == nullptr && (p.add == nullptr || p.add != p.out);
+}
+
+template <int MODE>
+static void launch_c64(const GemmNTParams& p, hipStream_t st) {
+  C64Args ca{};
+  const int batch = p.M / (p.OH * p.OW);
+  ca.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * 64 * 2);
+  ca.w_bytes = (unsigned)((size_t)64 * 576 * 2);
+  ca.W = p.OW;
+  ca.H = p.OH;
+  ca.tiles = (p.M + c64::BM - 1) / c64::BM;
+  static const int dbg = getenv("AVT_C64_DBG") ? atoi(getenv("AVT_C64_DBG")) : 0;
+  ca.dbg = dbg;
+  for (int r = 0; r < 3; ++r)
+    for (int s = 0; s < 3; ++s) {
+      const int t = r * 3 + s;
+      const int dy = MODE == MODE_FWD ? r - 1 : 1 - r, dx = MODE == MODE_FWD ? s - 1 : 1 - s;
+      ca.tap_dy[t] = dy;
+      ca.tap_dx[t] = dx;
+    }
+  int grid = num_cus();
+  if (grid > ca.tiles) grid = ca.tiles;
+  if (grid <= 0) return;
+  if constexpr (MODE == MODE_DGRAD) {
+    if (p.add != nullptr && p.amask != nullptr) {
+      hipLaunchKernelGGL((conv_c64_kernel<MODE, 2>), dim3(grid), dim3(256), 0, st, p, ca);
+      return;
+    }
+    if (p.add != nullptr) {
+      hipLaunchKernelGGL((conv_c64_kernel<MODE, 1>), dim3(grid), dim3(256), 0, st, p, ca);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv_c64_kernel<MODE, 0>), dim3(grid), dim3(256), 0, st, p, ca);
+}
+
 template <int MODE, int CVEC, int BM, int BN>
 static void launch_nt(const GemmNTParams& p, hipStream_t st) {
+  if (CVEC == 8 && c64_eligible(p)) {
+    launch_c64<MODE>(p, st);
+    return;
+  }
   if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && g_nt64_config == 1 &&
       p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
     if (p.Ng % 128 == 0) {

@@ -75,6 +75,10 @@ int avt_set_nt64_config(int cfg);
  * run on the halo-reuse kernel (each input pixel moved to LDS once per 64-channel chunk instead of once
  * per tap); 0: tap-gather kernel everywhere; 2: also the 8-wave halo forms for W <= 79 — an A/B knob */
 int avt_set_halo(int on);
+/* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
+ * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
+ * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */
+int avt_set_c64(int on);
 /* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
  * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */

@@ -211,6 +211,53 @@ def test_halo_matches_gather(case):
         torch.testing.assert_close(a1[:, 0], a0[:, 0], rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("N,H,W", [(3, 56, 56), (2, 65, 75), (21, 56, 56), (1, 7, 95)])
+def test_c64_matches_gather(N, H, W):
+    """Layer-1 persistent resident-weight kernel (avt_set_c64) vs the tap-gather kernel: fwd + BN partials,
+    dgrad, dgrad + add, dgrad + masked add; partial last tiles and more tiles than CUs (N=21 at 56^2)."""
+    C = K = 64
+    x = _rand_act(N, H, W, C, 51).relu().to(DEV)
+    g = torch.Generator().manual_seed(52)
+    w = (torch.randn(K, 3, 3, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, 9 * C)
+    dy = _rand_act(N, H, W, K, 53).to(DEV)
+    add = _rand_act(N, H, W, C, 54).to(DEV)
+    bits = torch.randint(0, 256, (N * H * W * C // 8,), generator=torch.Generator().manual_seed(55),
+                         dtype=torch.uint8).to(DEV)
+    outs = []
+    try:
+        for on in (0, 1):
+            call("avt_set_c64", on)
+            y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+            acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, 3, 3, 1, 1, 9 * C, S())
+            dx, dxa, dxm = (torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, 3, 3, 1, 1, S())
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dxa), P(add), N, H, W, C, K, 3, 3, 1, 1, S())
+            call("avt_conv2d_dgrad_mask", P(dy), P(wt), P(dxm), P(add), P(bits), N, H, W, C, K, 3, 3, 1, 1, S())
+            torch.cuda.synchronize()
+            a = acc.view(-1, K, 3).sum(0)
+            n = N * H * W
+            outs.append((y.float(), dx.float(), dxa.float(), dxm.float(), a[:, 0], a[:, 1] + a[:, 2] - a[:, 0] ** 2 / n))
+    finally:
+        call("avt_set_c64", 1)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2).cpu(), w.to(torch.bfloat16).double().permute(0, 3, 1, 2).cpu(),
+                   padding=1).permute(0, 2, 3, 1)
+    assert rel_err(outs[1][0], ref) < 8e-3
+    refd = torch.nn.grad.conv2d_input((N, C, H, W), w.to(torch.bfloat16).double().permute(0, 3, 1, 2).cpu(),
+                                      dy.double().permute(0, 3, 1, 2).cpu(), padding=1).permute(0, 2, 3, 1)
+    assert rel_err(outs[1][1], refd) < 8e-3
+    keep = ((bits.cpu().long().unsqueeze(1) >> torch.arange(8)) & 1).bool().reshape(N, H, W, C)
+    assert rel_err(outs[1][2], refd + add.double().cpu()) < 8e-3
+    assert rel_err(outs[1][3], refd + torch.where(keep, add.cpu(), torch.zeros_like(add.cpu())).double()) < 8e-3
+    for k in range(4):  # same products, another fp32 summation order: bf16 outputs mostly bit-equal
+        assert rel_err(outs[1][k], outs[0][k]) < 1e-2
+        assert (outs[1][k] - outs[0][k]).abs().gt(0).float().mean().item() < 0.1
+    rows = ref.reshape(-1, K)
+    torch.testing.assert_close(outs[1][4].cpu(), rows.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(outs[1][5].cpu(), ((rows - rows.mean(0)) ** 2).sum(0), rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("cin,cp,H,W,N", [(3, 4, 20, 22, 2), (1, 1, 21, 17, 2), (3, 4, 224, 224, 2),
                                            (1, 1, 257, 300, 2), (3, 4, 224, 224, 7), (1, 1, 257, 300, 16)])
 def test_stem_fwd_wgrad(cin, cp, H, W, N):
@@ -771,6 +818,14 @@ def test_conv_dgrad_bn_epilogue(case, mode):
     (xc, scale, shift) or read from y) and accumulates that BN's backward reductions (and a second
     BN's) -- bitwise the masked plain-dgrad result, sums == fp64 sums of it; then
     avt_bn_bwd_premasked consumes the accumulator like avt_bn_bwd."""
+    call("avt_set_c64", 0)  # the epilogue lives in the tap-gather / halo kernels: compare like with like
+    try:
+        _dgrad_bn_epilogue(case, mode)
+    finally:
+        call("avt_set_c64", 1)
+
+
+def _dgrad_bn_epilogue(case, mode):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     dy = _rand_act(N, Pq, Qq, K, 15)
