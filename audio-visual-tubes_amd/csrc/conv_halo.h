@@ -28,7 +28,7 @@ struct HaloArgs {
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
 // EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false>
-__global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p, HaloArgs ha) {
+__global__ __launch_bounds__(WM * WN * 64, 2) void conv_halo_kernel(GemmNTParams p, HaloArgs ha) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int BK = 64, RB = 128, RPI = 8;  // 64 channels = one 128-B row; 8 rows per 1 KiB DMA
@@ -38,17 +38,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
   static_assert(NSTB == 2 || NSTB == 3, "NSTB");
   constexpr int NPIECE = 10 - NSTB;  // patch pieces ride on taps NSTB-1 .. 8
   constexpr int AP = (PINSTR + NPIECE * NW - 1) / (NPIECE * NW);  // patch instructions per wave per piece
-  constexpr int ABUF = PRMAX * RB;
+  constexpr int ABUF = PRMAX * RB + 1024;  // a patch buffer + 8 zero rows (masked taps read them)
   constexpr int BSTAGE = BN * RB;
   constexpr int CT_LD = BN + 8;
   constexpr int EPI_BYTES = BM * CT_LD * 2;
   constexpr int MAIN = 2 * ABUF + NSTB * BSTAGE;
   constexpr int SMEM = (MAIN > EPI_BYTES ? MAIN : EPI_BYTES);
   static_assert(PRMAX % RPI == 0, "PRMAX");
-  // + 1 KiB of zeros: the row masked taps read, and the sink of the constant-count dummy DMAs
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + 1024 + 2 * WM * BN * 4];
-  char* zrow = smem + SMEM;
-  float* red = reinterpret_cast<float*>(smem + SMEM + 1024);  // [2][WM][BN] epilogue scratch
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * WM * BN * 4];
+  char* zrow = smem + PRMAX * RB;  // buffer 0's zero rows: also the sink of the constant-count dummy DMAs
+  float* red = reinterpret_cast<float*>(smem + SMEM);  // [2][WM][BN] epilogue scratch
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -63,7 +62,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
   const int nchunk = p.IC / BK;
   const int S = nchunk * 9;
 
-  if (tid < 64) reinterpret_cast<u32x4*>(zrow)[tid] = u32x4{0u, 0u, 0u, 0u};
+  if (tid < 128) reinterpret_cast<u32x4*>(zrow + (tid >> 6) * ABUF)[tid & 63] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.act, (short)0, (int)ha.act_bytes, 0x00020000);
@@ -87,13 +86,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
     const int lc = pchunk ^ ((row >> 1) & 7);
     b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
   }
-  // tap table in VGPR lanes (read with v_readlane: no scalar-memory wait in the loop)
-  int lane_tapw = 0, lane_disp = 0;
-  if (lane < 9) {
-    lane_tapw = ha.tap_w[lane] * p.IC * 2;
-    lane_disp = ha.tap_disp[lane];
-  }
-
   // ---- fragment rows of this lane: rows wm*(BM/WM) + i*32 + (lane & 31); per row a 9-bit tap mask ----
   const int frow = lane & 31, fhalf = lane >> 5;
   unsigned fmask[TM];
@@ -113,31 +105,46 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
     }
     fmask[i] = mk;
   }
+  // ---- per-lane A row address of every (tap, row block), relative to the patch buffer: masked taps read
+  //      the buffer's zero rows at the bank position the real row would have; the fragment-chunk swizzle
+  //      g = fhalf ^ (pr >> 1) & 7 sits in bits 4-6 (rows are 128 B), so a k-step's chunk is one XOR.
+  //      B: per (column block, k-step) offset in a ring stage.  With the tap loop unrolled the k loop is
+  //      ds_read + MFMA (tap, stage and buffer are compile-time; a rolled (chunk, tap) loop spent ~11
+  //      other instructions per MFMA) ----
+  unsigned arow[9][TM];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int pr = wm * (BM / WM) + i * 32 + frow + pre + ha.tap_disp[t];
+      const bool v = (fmask[i] >> t) & 1u;
+      arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((fhalf ^ ((pr >> 1) & 7)) << 4));
+    }
+  int boffs[TN][BK / 16];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) boffs[j][ks] = swz_rb<RB>(wn * (BN / WN) + j * 32 + frow, ks * 2 + fhalf);
 
-  // ---- issue of step j: weight tile (tap t, chunk c) into ring stage j % NSTB, and for t >= 2 one
-  //      piece of chunk c+1's patch into patch buffer (c+1) & 1 ----
-  int is_c = 0, is_t = 0;  // (chunk, tap) of the next step to issue (wave-uniform)
-  auto issue = [&](int j) {
-    char* Bs = smem + 2 * ABUF + (j % NSTB) * BSTAGE;
-    const bool live = j < S;
-    const int t = live ? is_t : 0;
-    const unsigned boff = (unsigned)(__builtin_amdgcn_readlane(lane_tapw, t) + is_c * BK * 2);
+  // ---- issue of step (chunk cn, tap tn): weight tile into ring stage (cn*9+tn) % NSTB, and for tn >=
+  //      NSTB-1 one piece of chunk cn+1's patch into patch buffer (cn+1) & 1 (which held chunk cn-1, whose
+  //      last reader has passed) ----
+  auto issue = [&](int cn, int tn, int stage) {
+    char* Bs = smem + 2 * ABUF + stage * BSTAGE;
+    const bool live = cn < nchunk;
+    const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + cn * BK) * 2);
 #pragma unroll
     for (int i = 0; i < BR; ++i) buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
-    if (is_t >= NSTB - 1) {  // the buffer (c+1)&1 held chunk c-1, whose last reader has passed
-      char* Ab = smem + ((is_c + 1) & 1) * ABUF;
-      const bool alive = live && is_c + 1 < nchunk;
+    if (tn >= NSTB - 1) {
+      char* Ab = smem + ((cn + 1) & 1) * ABUF;
+      const bool alive = live && cn + 1 < nchunk;
 #pragma unroll
       for (int a = 0; a < AP; ++a) {
-        const int q = ((is_t - (NSTB - 1)) * AP + a) * NW + wid;  // pieces 0..6 of the patch
+        const int q = ((tn - (NSTB - 1)) * AP + a) * NW + wid;  // pieces 0..6 of the patch
         const bool inrange = q < PINSTR;
         // out-of-range instructions still issue (constant vmcnt): zeros into the zero area
-        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, is_c + 1) : kOOB);
+        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, cn + 1) : kOOB);
       }
-    }
-    if (++is_t == 9) {
-      is_t = 0;
-      ++is_c;
     }
   };
 
@@ -152,59 +159,57 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_halo_kernel(GemmNTParams p,
   // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2
   for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, 0));
 #pragma unroll
-  for (int j = 0; j < NSTB - 1; ++j) issue(j);
+  for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
   constexpr int KS = BK / 16;
   bf16x8 af[2][TM], bfr[2][TN];
-  int rowaddr[TM], rowsw[TM];
-  for (int s = 0; s < S; ++s) {
-    const int c = s / 9, t = s - c * 9;
-    // step s has landed once only step s+1's loads may be outstanding (issued after it)
-    if constexpr (NSTB == 2) {
-      wait_vmcnt<0>();
-    } else {
-      const int tn = t + 1 == 9 ? 0 : t + 1;
-      if (tn >= NSTB - 1)
-        wait_vmcnt<BR + AP>();
-      else
-        wait_vmcnt<BR>();
-    }
-    __builtin_amdgcn_s_barrier();
-    const char* Ab = smem + (c & 1) * ABUF;
-    const char* Bs = smem + 2 * ABUF + (s % NSTB) * BSTAGE;
-    const int disp = __builtin_amdgcn_readlane(lane_disp, t);
+  for (int c = 0; c < nchunk; ++c) {
+    const char* Ab = smem + (c & 1) * ABUF;  // patch buffer of this chunk
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int pr = wm * (BM / WM) + i * 32 + frow + pre + disp;
-      const bool v = (fmask[i] >> t) & 1u;
-      // masked taps read zeros from the zero area, at the bank position the real row would have
-      rowaddr[i] = (v ? (int)(Ab - smem) : SMEM - (pr & ~7) * RB) + pr * RB;
-      rowsw[i] = (pr >> 1) & 7;
-    }
-    auto load_frags = [&](int ks, int buf) {
+    for (int t = 0; t < 9; ++t) {
+      {
+        // step s = c*9 + t: its stage is s % NSTB -- (c + t) % 2 for NSTB 2 (9 odd), t % 3 for 3
+        const int stage = NSTB == 2 ? (c + t) & 1 : t % 3;
+        // step s has landed once only step s+1's loads may be outstanding (issued after it)
+        if constexpr (NSTB == 2) {
+          wait_vmcnt<0>();
+        } else {
+          const int tn = t + 1 == 9 ? 0 : t + 1;
+          if (tn >= NSTB - 1)
+            wait_vmcnt<BR + AP>();
+          else
+            wait_vmcnt<BR>();
+        }
+        __builtin_amdgcn_s_barrier();
+        const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
+        auto load_frags = [&](int ks, int buf) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[buf][i] = *reinterpret_cast<const bf16x8*>(smem + rowaddr[i] + (((ks * 2 + fhalf) ^ rowsw[i]) << 4));
+          for (int i = 0; i < TM; ++i)
+            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * (BN / WN) + j * 32 + frow;
-        bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + swz_rb<RB>(row, ks * 2 + fhalf));
+          for (int j = 0; j < TN; ++j) bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
+        };
+        load_frags(0, 0);
+        {  // the ring stage read at step s-1; every wave has passed that
+          const int tn = t + NSTB - 1 >= 9 ? t + NSTB - 1 - 9 : t + NSTB - 1;
+          const int cn = t + NSTB - 1 >= 9 ? c + 1 : c;
+          const int stn = NSTB == 2 ? (stage ^ 1) : (stage + 2) % 3;
+          issue(cn, tn, stn);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            load_frags(ks + 1, (ks + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+          if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
+        }
       }
-    };
-    load_frags(0, 0);
-    issue(s + NSTB - 1);  // the ring stage read at step s-1; every wave has passed that
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) {
-        load_frags(ks + 1, (ks + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
-      if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
     }
   }
   wait_vmcnt<0>();
