@@ -708,7 +708,10 @@ static bool halo_eligible(const GemmNTParams& p) {
       p.IH != p.OH || p.IW != p.OW)
     return false;
   if (h == 2) return 256 + 2 * p.OW + 2 <= kHaloPR && (p.Ng % 128 == 0 || p.Ng == 64);  // 8-wave forms (A/B)
-  return p.Ng % 128 == 0 && 128 + 2 * p.OW + 2 <= 168;                                // W <= 19
+  // W <= 19 (layer3/4): 4-wave 128x128; W <= 79 (layer2): 8-wave 256x128 (measured with the unrolled tap
+  // loop: audio layer2 +6-10 % at B=128 and +28 % at B=32 over the tap gather, vision layer2 +0-6 %)
+  static const int l2 = getenv("AVT_HALO_L2") ? atoi(getenv("AVT_HALO_L2")) : 1;  // A/B: 0 = layer2 on the tap gather
+  return p.Ng % 128 == 0 && (128 + 2 * p.OW + 2 <= 168 || (l2 && 256 + 2 * p.OW + 2 <= kHaloPR));
 }
 
 // Small GEMMs (a few clips per GPU: BASELINE configs[2] runs 32 per GPU): a tile grid that leaves
@@ -820,12 +823,16 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
     // measured (tools/conv_bench.py): the 4-wave 128 x 128 form at 2 blocks per CU beats the tap
     // gather on layer3/4 (W <= 19: +2..16 %); the 8-wave 256-row forms a patch of the wider layer1/2
     // images needs (1 block per CU) lose to it (-1..-20 %), so those keep the tap-gather kernel
-    if (g_halo == 2 && p.Ng % 128 == 0)
-      launch_halo<MODE, 4, 2, 2, 2>(p, st);  // 256 x 128, 8 waves (A/B only)
+    if (p.Ng % 128 == 0 && (g_halo == 2 || 128 + 2 * p.OW + 2 > 168)) {
+      if (256 + 2 * p.OW + 2 <= 336)
+        launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
+      else
+        launch_halo<MODE, 4, 2, 2, 2, 2>(p, st);  // W <= 79: 2 weight stages to fit the 416-row patches
+    }
     else if (g_halo == 2)
       launch_halo<MODE, 4, 2, 2, 1>(p, st);  // 256 x 64, 8 waves (A/B only)
     else
-      launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st);  // 128 x 128, 4 waves, 77 KB LDS: 2 blocks per CU
+      launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st);  // 128 x 128, 4 waves, 80 KB LDS: 2 blocks per CU
     return;
   }
   if (CVEC == 8 && conv_variant() == 1) {

@@ -45,6 +45,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_halo_kernel(GemmNTParams
   constexpr int MAIN = 2 * ABUF + NSTB * BSTAGE;
   constexpr int SMEM = (MAIN > EPI_BYTES ? MAIN : EPI_BYTES);
   static_assert(PRMAX % RPI == 0, "PRMAX");
+  static_assert(SMEM + 2 * WM * BN * 4 <= 160 * 1024, "LDS budget of a CU");
   __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * WM * BN * 4];
   char* zrow = smem + PRMAX * RB;  // buffer 0's zero rows: also the sink of the constant-count dummy DMAs
   float* red = reinterpret_cast<float*>(smem + SMEM);  // [2][WM][BN] epilogue scratch

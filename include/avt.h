@@ -71,9 +71,10 @@ int avt_set_conv_variant(int variant);
  * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
  * — an A/B knob */
 int avt_set_nt64_config(int cfg);
-/* 1 (default; env AVT_HALO): 3x3 stride-1 fwd/dgrad with C % 64 == 0, K % 128 == 0 and W <= 19 (layer3/4)
- * run on the halo-reuse kernel (each input pixel moved to LDS once per 64-channel chunk instead of once
- * per tap); 0: tap-gather kernel everywhere; 2: also the 8-wave halo forms for W <= 79 — an A/B knob */
+/* 1 (default; env AVT_HALO): 3x3 stride-1 fwd/dgrad with C % 64 == 0 and K % 128 == 0 run on the halo-reuse
+ * kernel (each input pixel moved to LDS once per 64-channel chunk instead of once per tap): 4-wave 128x128
+ * tiles for W <= 19 (layer3/4), 8-wave 256x128 tiles for W <= 79 (layer2); 0: tap-gather kernel everywhere;
+ * 2: the 8-wave forms for every width (and 256x64 for K = 64) — an A/B knob */
 int avt_set_halo(int on);
 /* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per

@@ -818,11 +818,15 @@ def test_conv_dgrad_bn_epilogue(case, mode):
     (xc, scale, shift) or read from y) and accumulates that BN's backward reductions (and a second
     BN's) -- bitwise the masked plain-dgrad result, sums == fp64 sums of it; then
     avt_bn_bwd_premasked consumes the accumulator like avt_bn_bwd."""
-    call("avt_set_c64", 0)  # the epilogue lives in the tap-gather / halo kernels: compare like with like
+    # the epilogue lives in the tap-gather / halo kernels, which the small-tile path never picks for it:
+    # compare like with like
+    call("avt_set_c64", 0)
+    call("avt_set_small_tiles", 0)
     try:
         _dgrad_bn_epilogue(case, mode)
     finally:
         call("avt_set_c64", 1)
+        call("avt_set_small_tiles", 1)
 
 
 def _dgrad_bn_epilogue(case, mode):

@@ -13,8 +13,8 @@ import json
 import sys
 from collections import defaultdict
 
-CONV = ("conv_nt_pipe_kernel", "conv_tn_pipe_kernel", "gemm_nt_kernel", "gemm_tn_kernel",
-        "wgrad_slab_reduce_kernel")
+CONV = ("avt::conv_", "gemm_nt_kernel", "gemm_tn_kernel", "wgrad_slab_reduce_kernel")  # every conv kernel
+BN = ("avt::bn_", "avt::stem_bn", "avt::stem_maxpool")
 
 
 def load(d, ctr):
@@ -46,6 +46,9 @@ def main():
             conv_rd += rd
             conv_wr += wr
             conv_n += n
+    bn_b = sum(rd + wr for k, n, rd, wr in rows if any(c in k for c in BN))
+    tot_b = sum(rd + wr for k, n, rd, wr in rows)
+    print(f"step total: {tot_b / 1e9 / steps:.3f} GB/step; BN family {bn_b / 1e9 / steps:.3f} GB/step")
     for k, n, rd, wr in rows[:40]:
         print(f"{(rd + wr) / 1e9 / steps:8.3f} GB/step  read {rd / 1e9 / steps:7.3f}  write {wr / 1e9 / steps:7.3f}  "
               f"n={n / steps:6.1f}/step  {k[:90]}")
@@ -63,6 +66,7 @@ def main():
                    "conv_dispatches_per_step": conv_n / steps, "conv_read_bytes_per_step": conv_rd / steps,
                    "conv_write_bytes_per_step": conv_wr / steps,
                    "conv_bytes_per_dispatch": (conv_rd + conv_wr) / max(conv_n, 1),
+                   "step_bytes": tot_b / steps, "bn_family_bytes_per_step": bn_b / steps,
                    "per_kernel": {k[:120]: {"dispatches_per_step": n / steps, "read_bytes_per_step": rd / steps,
                                             "write_bytes_per_step": wr / steps} for k, n, rd, wr in rows}},
                   open(out, "w"), indent=1)
