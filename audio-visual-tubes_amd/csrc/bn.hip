@@ -561,6 +561,15 @@ __global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
   const int rowg = Q * C * 2, rowi = Q * C;  // bytes of one pooled row of gy / argmax
   bf16_t* lg = reinterpret_cast<bf16_t*>(lds);
   unsigned char* li = reinterpret_cast<unsigned char*>(lds + 2 * rowg);
+  // the pre-activations of this thread's (<= kStemItems) items are loaded first: they do not depend on
+  // the staged rows, so their HBM latency overlaps the staging and its barrier
+  constexpr int kStemItems = 6;
+  u32x4 cx[kStemItems];
+#pragma unroll
+  for (int j = 0; j < kStemItems; ++j) {
+    const int t = threadIdx.x + 256 * j;
+    if (t < W * cv) cx[j] = *reinterpret_cast<const u32x4*>(c + ((size_t)row * W) * C + (size_t)t * 8);
+  }
   for (int k = 0; k < np; ++k) {
     const size_t prow = (size_t)n * P + p0 + k;
     const u32x4* sg = reinterpret_cast<const u32x4*>(gy + prow * Q * C);
@@ -570,15 +579,6 @@ __global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
   }
   __syncthreads();
   const int k1r = p_two ? 1 : 0;  // LDS row of the second window row (aliases the first if none)
-  // the pre-activations of this thread's (<= kStemItems) items are loaded before any is used:
-  // enough 16-B loads in flight per CU to stream c at HBM rate
-  constexpr int kStemItems = 6;
-  u32x4 cx[kStemItems];
-#pragma unroll
-  for (int j = 0; j < kStemItems; ++j) {
-    const int t = threadIdx.x + 256 * j;
-    if (t < W * cv) cx[j] = *reinterpret_cast<const u32x4*>(c + ((size_t)row * W) * C + (size_t)t * 8);
-  }
 #pragma unroll
   for (int j = 0; j < kStemItems; ++j) {
     const int t = threadIdx.x + 256 * j;
