@@ -16,6 +16,10 @@
  *   avt_maxpool3s2_fwd/bwd       nn.MaxPool2d(3, 2, 1) (models/base_models.py:143, 203)
  *   avt_stem_*                   stem bn1 -> relu -> maxpool fused fwd/bwd (models/base_models.py:200-203)
  *   avt_bn_relu_bwd              BasicBlock bn1+relu backward, mask from the pre-activation (base_models.py:47-48)
+ *   avt_bn_apply_mask,           BasicBlock output relu(bn2(c2) + residual) (base_models.py:64-67) with its ReLU
+ *   avt_bn_bwd_mask,             mask kept as bits; the backward of bn2 (+ downsample.1) from those bits, and the
+ *   avt_conv2d_dgrad_mask        identity block's input gradient dgrad(conv1) + g * mask without a stored g'
+ *   avt_set_c64 / avt_set_halo   A/B knobs of the layer-1 resident-weight and halo-reuse conv kernels
  *   avt_audio_pool_norm_fwd/bwd  nn.AdaptiveMaxPool2d((1,1)) + F.normalize(dim=1) (model.py:96, 120-122)
  *   avt_hardway_fwd/bwd          AVENet.forward head: normalize, A/A0 einsums, sigmoid trimap,
  *                                sim1/sim/sim2, logits/0.07, weighted_A (model.py:114-154);
