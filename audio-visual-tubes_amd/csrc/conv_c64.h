@@ -25,7 +25,7 @@
 
 namespace c64 {
 constexpr int BM = 256;                 // output pixels per tile
-constexpr int NWAVE = 4;
+constexpr int NWMAX = 8;                // waves per block: 4 (64-row wave tiles) or 8 (32-row, two per SIMD)
 constexpr int KTOT = 9 * 64;            // GEMM K: (tap, channel)
 constexpr int WROW = KTOT * 2;          // bytes per resident weight row (1152)
 constexpr int WBYTES = 64 * WROW;       // 73,728
@@ -34,11 +34,9 @@ constexpr int RB = 64;                  // bytes per patch row of a 32-channel h
 constexpr int PBYTES = PRMAX * RB;      // 26,624 patch bytes per half-buffer ...
 constexpr int SLOT = PBYTES + 1024;     // ... + 16 zero rows (masked taps): 27,648
 constexpr int PINSTR = PRMAX / 16;      // 26 LDS-DMA instructions (16 rows x 64 B) per half
-constexpr int PI = (PINSTR + NWAVE - 1) / NWAVE;  // 7 per wave (those past PINSTR load zeros into the zero rows)
-constexpr int SPW = 32;                 // epilogue stores per wave and tile (4 accumulators x 8 pairs)
 constexpr int WOFF = 2 * SLOT;          // 55,296: resident weights (ds_read immediates stay < 64 KiB)
-constexpr int ROFF = WOFF + WBYTES;     // [2][4][64] floats: epilogue reduction scratch
-constexpr int SMEM = ROFF + 2 * NWAVE * 64 * 4;    // 131,072 B
+constexpr int ROFF = WOFF + WBYTES;     // [2][NW][64] floats: epilogue reduction scratch
+constexpr int SMEM = ROFF + 2 * NWMAX * 64 * 4;    // 133,120 B
 static_assert(PINSTR * 16 == PRMAX && SMEM <= 160 * 1024 && WOFF + 8 * 128 + 1024 < 65536, "LDS layout");
 }  // namespace c64
 
@@ -55,10 +53,16 @@ __device__ __forceinline__ float c64_swap1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
-// ADD: 0 none, 1 dx = dgrad + add, 2 dx = dgrad + add * mask bits
-template <int MODE, int ADD>
-__global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Args ca) {
+// ADD: 0 none, 1 dx = dgrad + add, 2 dx = dgrad + add * mask bits.  NWAVE 4: each wave a 64x64 sub-tile
+// (TM = 2); NWAVE 8: 32x64 (TM = 1), two waves per SIMD to cover each other's non-MFMA issue
+template <int MODE, int ADD, int NWAVE = 4>
+__global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p, C64Args ca) {
   using namespace c64;
+  constexpr int TM = 4 / (NWAVE / 2) ;     // 32-row accumulator blocks per wave: 2 (4 waves) / 1 (8 waves)
+  constexpr int WR = TM * 32;              // rows per wave
+  constexpr int PI = (PINSTR + NWAVE - 1) / NWAVE;  // DMA instructions per wave and half (past PINSTR: zeros)
+  constexpr int SPW = TM * 2 * 8;          // epilogue stores per wave and tile (TM x 2 accumulators x 8 pairs)
+  static_assert(TM * 32 * NWAVE == BM, "wave rows");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   float* red = reinterpret_cast<float*>(smem + ROFF);
 
@@ -81,7 +85,7 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
       __builtin_amdgcn_make_buffer_rsrc((void*)p.out, (short)0, (int)((unsigned)p.M * 128u), 0x00020000);
 
   // ---- resident weights: row n (output channel of the GEMM), 16-B chunk q stored at q ^ ((n>>1)&7) ----
-  for (int idx = tid; idx < 64 * (WROW / 16); idx += 256) {
+  for (int idx = tid; idx < 64 * (WROW / 16); idx += NWAVE * 64) {
     const int n = idx / (WROW / 16), q = idx - n * (WROW / 16);
     const u32x4 v = *reinterpret_cast<const u32x4*>(p.wmat + (size_t)n * KTOT + q * 8);
     *reinterpret_cast<u32x4*>(smem + WOFF + n * WROW + ((q ^ ((n >> 1) & 7)) << 4)) = v;
@@ -112,12 +116,12 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
 
   // ---- A addresses: rel[t][i][ks] = byte offset in a half-buffer of the 16-B fragment chunk of tap t,
   //      row block i, k-step ks (valid taps); masked taps read the zero rows at the same bank position ----
-  unsigned relv[9][2][2];
+  unsigned relv[9][TM][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int pr = wid * 64 + i * 32 + frow + pre + ca.tap_dy[t] * W + ca.tap_dx[t];
+    for (int i = 0; i < TM; ++i) {
+      const int pr = wid * WR + i * 32 + frow + pre + ca.tap_dy[t] * W + ca.tap_dx[t];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) relv[t][i][ks] = (unsigned)(pr * RB + (((ks * 2 + fhalf) ^ ((pr >> 2) & 3)) << 4));
     }
@@ -146,10 +150,10 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
   for (int it = 0; tile < thi; tile += nbx, ++it) {
     const int m0 = tile * BM;
     // border mask of this tile's fragment rows -> the A offsets of the tile
-    unsigned rel[9][2][2];
+    unsigned rel[9][TM][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + wid * 64 + i * 32 + frow;
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wid * WR + i * 32 + frow;
       const bool ok = m < p.M;
       const int mm = ok ? m : 0;
       const int n = mm / hw, rem = mm - n * hw;
@@ -162,9 +166,9 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
         for (int ks = 0; ks < 2; ++ks) rel[t][i][ks] = v ? relv[t][i][ks] : ((relv[t][i][ks] & 1023u) | (unsigned)PBYTES);
       }
     }
-    f32x16 acc[2][2];
+    f32x16 acc[TM][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -182,12 +186,12 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
       else
         issue_half(tile + nbx, 0);
       // 18 k-steps (tap t, ks): k = t*64 + half*32 + ks*16; fragments of step s+1 read while step s multiplies
-      bf16x8 af[2][2], bfr[2][2];
+      bf16x8 af[2][TM], bfr[2][2];
       const char* abuf = smem + half * SLOT;
       auto load_frags = [&](int s, int buf) {
         const int t = s >> 1, ks = s & 1;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[buf][i] = *reinterpret_cast<const bf16x8*>(abuf + rel[t][i][ks]);
+        for (int i = 0; i < TM; ++i) af[buf][i] = *reinterpret_cast<const bf16x8*>(abuf + rel[t][i][ks]);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           bfr[buf][j] = *reinterpret_cast<const bf16x8*>(smem + WOFF + 128 * t + bb[half][ks][j]);
@@ -200,7 +204,7 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][i], bfr[s & 1][j], acc[i][j], 0, 0, 0);
@@ -215,10 +219,10 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
       for (int j = 0; j < 2; ++j) {
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const int r = wid * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+            const int r = wid * WR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
             if (r < rows_valid) s += acc[i][j][v];
           }
         s += __shfl_xor(s, 32, 64);
@@ -228,18 +232,21 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = j * 32 + frow;
-        const float mean = (red[c] + red[64 + c] + red[128 + c] + red[192 + c]) / (float)rows_valid;
+        float tot = 0.f;
+#pragma unroll
+        for (int k = 0; k < NWAVE; ++k) tot += red[k * 64 + c];
+        const float mean = tot / (float)rows_valid;
         float q = 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int v = 0; v < 16; ++v) {
-            const int r = wid * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+            const int r = wid * WR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
             const float d = acc[i][j][v] - mean;
             if (r < rows_valid) q += d * d;
           }
         q += __shfl_xor(q, 32, 64);
-        if (lane < 32) red[256 + wid * 64 + c] = q;
+        if (lane < 32) red[NWAVE * 64 + wid * 64 + c] = q;
       }
       __syncthreads();
       if (tid < 64) {
@@ -247,7 +254,7 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
 #pragma unroll
         for (int k = 0; k < NWAVE; ++k) {
           s += (double)red[k * 64 + tid];
-          m2 += (double)red[256 + k * 64 + tid];
+          m2 += (double)red[NWAVE * 64 + k * 64 + tid];
         }
         double* a = p.stats + ((size_t)(tile % AVT_BN_SLOTS) * p.Ng + tid) * 3;
         atomicAdd(a + 0, s);
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
     // Per 32x32 accumulator the 8 `add` words (and mask bytes) are loaded together before any is used.
     const bool odd = lane & 1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = j * 32 + (frow & ~1);
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(256, 1) void conv_c64_kernel(GemmNTParams p, C64Arg
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int v = 2 * u;
-          const int r = wid * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf + (odd ? 1 : 0);
+          const int r = wid * WR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf + (odd ? 1 : 0);
           okv[u] = r < rows_valid;
           offs[u] = (size_t)(m0 + (okv[u] ? r : 0)) * 64 + c;  // element offset of the pair
           if (ADD) av[u] = *reinterpret_cast<const unsigned*>(p.add + offs[u]);
