@@ -48,6 +48,7 @@ SIGNATURES = {
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
     "avt_set_c64": (_I, [_I]),
+    "avt_set_s2_dgrad_one": (_I, [_I]),
     "avt_set_stem_kernel": (_I, [_I]),
     "avt_set_stem_wgrad": (_I, [_I]),
     "avt_set_nt128_config": (_I, [_I]),

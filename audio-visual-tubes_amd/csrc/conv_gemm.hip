@@ -546,6 +546,15 @@ static int c64_enabled() {
   return g_c64;
 }
 
+static int g_s2_one = -1;  // stride-2 dgrad parity classes in one launch: -1 = env AVT_S2_ONE (default 1)
+static int s2_one() {
+  if (g_s2_one < 0) {
+    const char* e = getenv("AVT_S2_ONE");
+    g_s2_one = e ? atoi(e) : 1;
+  }
+  return g_s2_one;
+}
+
 static int g_conv_variant = -1;  // -1: read AVT_CONV_VARIANT once (0 = register-staged, 1 = LDS-DMA)
 static int conv_variant() {
   if (g_conv_variant < 0) {
@@ -566,6 +575,11 @@ extern "C" int avt_set_conv_variant(int v) {
 
 extern "C" int avt_set_c64(int on) {
   g_c64 = on ? 1 : 0;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_s2_dgrad_one(int on) {
+  g_s2_one = on ? 1 : 0;
   return AVT_OK;
 }
 
@@ -672,6 +686,53 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
   ta.cls = 1;
   ta.OHf = p.OH;
   ta.OWf = p.OW;
+  // one launch for all classes (no BN-backward epilogue): blocks of the classes with the most taps
+  // are dispatched first, and the classes' tails overlap instead of running as four short grids
+  if (s2_one() && p.bx == nullptr && p.R * p.S <= 9) {
+    struct Cls { int ph, pw, n, tiles; } cl[4];
+    int ncl = 0;
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        int n = 0;
+        for (int r = 0; r < p.R; ++r)
+          for (int s = 0; s < p.S; ++s) n += !(((ph + p.pad - r) & 1) || ((pw + p.pad - s) & 1));
+        const int m = batch * ((p.OH - ph + 1) / 2) * ((p.OW - pw + 1) / 2);
+        if (m == 0 || (n == 0 && p.add != nullptr && p.add == p.out)) continue;  // see below
+        cl[ncl++] = Cls{ph, pw, n, ((m + BM - 1) / BM) * (p.Ng / BN)};
+      }
+    for (int i = 1; i < ncl; ++i)  // most taps first (stable)
+      for (int j = i; j > 0 && cl[j].n > cl[j - 1].n; --j) std::swap(cl[j], cl[j - 1]);
+    NTPipeArgsV tc = ta;
+    tc.ncls = ncl;
+    tc.batch = batch;
+    tc.ntaps = 0;
+    int start = 0;
+    for (int k = 0; k < ncl; ++k) {
+      const int first = tc.ntaps;
+      for (int r = 0; r < p.R; ++r)
+        for (int s = 0; s < p.S; ++s) {
+          if (((cl[k].ph + p.pad - r) & 1) || ((cl[k].pw + p.pad - s) & 1)) continue;
+          tc.tap_w[tc.ntaps] = r * p.S + s;
+          tc.tap_dy[tc.ntaps] = (cl[k].ph + p.pad - r) / 2;
+          tc.tap_dx[tc.ntaps] = (cl[k].pw + p.pad - s) / 2;
+          ++tc.ntaps;
+        }
+      tc.cls_start[k] = start;
+      tc.cls_meta[k] = cl[k].n | first << 4 | cl[k].ph << 8 | cl[k].pw << 9;
+      start += cl[k].tiles;
+    }
+    if (ncl == 0 || start == 0) return;
+    tc.ph = cl[0].ph;  // ncls == 1: the plain class mode (then tc.ntaps == cl[0].n)
+    tc.pw = cl[0].pw;
+    GemmNTParams pc = p;
+    pc.OH = (p.OH - cl[0].ph + 1) / 2;
+    pc.OW = (p.OW - cl[0].pw + 1) / 2;
+    pc.M = batch * pc.OH * pc.OW;
+    if (ncl > 1) pc.M = start / (p.Ng / BN) * BM;  // launch_pipe_one's grid = start; each block takes its class's M
+    launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
+    return;
+  }
   for (int ph = 0; ph < 2; ++ph)
     for (int pw = 0; pw < 2; ++pw) {
       NTPipeArgsV tc = ta;

@@ -56,6 +56,11 @@ struct NTPipeArgsT {
   int cls;                // 1: rows are one parity class of a stride-2 dgrad output
   int ph, pw;             // that class
   int OHf, OWf;           // full output grid (class mode)
+  // ncls > 1: the parity classes of a stride-2 dgrad in ONE launch.  Blocks [cls_start[k],
+  // cls_start[k+1]) run class k; cls_meta[k] = ntaps | first tap << 4 | ph << 8 | pw << 9 (its taps
+  // are tap_*[first tap ..]); class k's grid is ((OHf - ph + 1) / 2) x ((OWf - pw + 1) / 2) per sample.
+  int ncls, batch;
+  int cls_start[4], cls_meta[4];
 };
 typedef NTPipeArgsT<9> NTPipeArgs;          // Conv2d (3x3 and 1x1)
 typedef NTPipeArgsT<kMaxTaps> NTPipeArgsV;  // Conv3d 3x3x3 and the folded 7x7 video stem
@@ -77,6 +82,12 @@ inline NTPipeArgs narrow_args(const NTPipeArgsV& v) {
   a.pw = v.pw;
   a.OHf = v.OHf;
   a.OWf = v.OWf;
+  a.ncls = v.ncls;
+  a.batch = v.batch;
+  for (int k = 0; k < 4; ++k) {
+    a.cls_start[k] = v.cls_start[k];
+    a.cls_meta[k] = v.cls_meta[k];
+  }
   return a;
 }
 
@@ -119,7 +130,24 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
   const int nnt = p.Ng / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int bid, ntaps = ta.ntaps, tb = 0, cph = ta.ph, cpw = ta.pw;
+  if (!VID && MODE == MODE_DGRAD && ta.ncls > 1) {  // block-uniform: this block's parity class
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      if (j < ta.ncls && (int)blockIdx.x >= ta.cls_start[j]) k = j;
+    const int meta = ta.cls_meta[k];
+    ntaps = meta & 15;
+    tb = (meta >> 4) & 15;
+    cph = (meta >> 8) & 1;
+    cpw = (meta >> 9) & 1;
+    p.OH = (ta.OHf - cph + 1) >> 1;
+    p.OW = (ta.OWf - cpw + 1) >> 1;
+    p.M = ta.batch * p.OH * p.OW;
+    bid = (int)blockIdx.x - ta.cls_start[k];  // heavy classes first in dispatch order; no XCD remap
+  } else {
+    bid = xcd_remap(blockIdx.x, gridDim.x);
+  }
   const int mt = bid / nnt, nt = bid - mt * nnt;
   const int m0 = mt * BM, n0 = nt * BN;
 
@@ -160,11 +188,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
       xb = ow;
     }
     mask_t mask = 0;
-    for (int t = 0; t < ta.ntaps; ++t) {
-      const int y = yb + ta.tap_dy[t], x = xb + ta.tap_dx[t];
+    for (int t = 0; t < ntaps; ++t) {
+      const int y = yb + ta.tap_dy[tb + t], x = xb + ta.tap_dx[tb + t];
       bool v = ok && y >= 0 && y < p.IH && x >= 0 && x < p.IW;
       if constexpr (VID) {
-        const int tt = ot + ta.tap_dt[t];
+        const int tt = ot + ta.tap_dt[tb + t];
         v = v && tt >= 0 && tt < p.IT;
       }
       mask |= (v ? (mask_t)1 : (mask_t)0) << t;
@@ -183,16 +211,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
   }
   const int cpt = p.IC / BK;  // k-tiles per tap
-  const int nkt = ta.ntaps * cpt;
+  const int nkt = ntaps * cpt;
 
   // Tap table in VGPRs: lane t (< ntaps) holds tap t's activation and weight byte offsets; the
   // k loop reads them with v_readlane (no scalar-memory load, hence no lgkmcnt wait that would
   // also drain the LDS fragment reads, on the loop's critical path).
   int lane_tapoff = 0, lane_tapw = 0;
-  if (lane < ta.ntaps) {
-    const int dt = VID ? ta.tap_dt[lane] : 0;
-    lane_tapoff = ((dt * p.IH + ta.tap_dy[lane]) * p.IW + ta.tap_dx[lane]) * p.IC * 2;
-    lane_tapw = ta.tap_w[lane] * p.IC * 2;
+  if (lane < ntaps) {
+    const int dt = VID ? ta.tap_dt[tb + lane] : 0;
+    lane_tapoff = ((dt * p.IH + ta.tap_dy[tb + lane]) * p.IW + ta.tap_dx[tb + lane]) * p.IC * 2;
+    lane_tapw = ta.tap_w[tb + lane] * p.IC * 2;
   }
 
   // incremental state of the next tile to issue (wave-uniform)
@@ -345,7 +373,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     const int m = m0 + r;
     const int n = m / hw, rem = m - n * hw;
     const int oh = rem / p.OW, ow = rem - oh * p.OW;
-    return ((size_t)n * ta.OHf + 2 * oh + ta.ph) * ta.OWf + 2 * ow + ta.pw;
+    return ((size_t)n * ta.OHf + 2 * oh + cph) * ta.OWf + 2 * ow + cpw;
   };
   epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, orow, reinterpret_cast<float*>(smem));
 }

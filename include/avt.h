@@ -20,6 +20,7 @@
  *   avt_bn_bwd_mask,             mask kept as bits; the backward of bn2 (+ downsample.1) from those bits, and the
  *   avt_conv2d_dgrad_mask        identity block's input gradient dgrad(conv1) + g * mask without a stored g'
  *   avt_set_c64 / avt_set_halo   A/B knobs of the layer-1 resident-weight and halo-reuse conv kernels
+ *   avt_set_s2_dgrad_one         A/B knob: the stride-2 dgrad's four parity classes in one launch
  *   avt_audio_pool_norm_fwd/bwd  nn.AdaptiveMaxPool2d((1,1)) + F.normalize(dim=1) (model.py:96, 120-122)
  *   avt_hardway_fwd/bwd          AVENet.forward head: normalize, A/A0 einsums, sigmoid trimap,
  *                                sim1/sim/sim2, logits/0.07, weighted_A (model.py:114-154);
@@ -84,6 +85,10 @@ int avt_set_halo(int on);
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
  * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */
 int avt_set_c64(int on);
+/* 1 (default; env AVT_S2_ONE): a stride-2 dgrad without the BN-backward epilogue runs its output parity
+ * classes (each with only the taps that reach it) as ONE launch, blocks of the classes with the most taps
+ * dispatched first; 0: one launch per class.  The results are bitwise identical (same tap order). */
+int avt_set_s2_dgrad_one(int on);
 /* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
  * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */

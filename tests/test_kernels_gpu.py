@@ -351,6 +351,40 @@ def test_conv_dgrad(case, tiles):
     assert torch.equal(dx3, dx4)
 
 
+@pytest.mark.parametrize("case", [(2, 9, 11, 64, 128, 3, 2, 1), (3, 7, 5, 128, 256, 1, 2, 0),
+                                  (32, 56, 56, 64, 128, 3, 2, 1), (32, 33, 38, 128, 256, 3, 2, 1),
+                                  (5, 65, 75, 64, 128, 1, 2, 0), (1, 2, 3, 64, 64, 3, 2, 1)])
+def test_strided_dgrad_one_launch(case, tiles):
+    """The stride-2 dgrad's parity classes in one launch (avt_set_s2_dgrad_one(1), the default) against one
+    launch per class: bitwise equal, with and without an accumulated add, and accumulating in place."""
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    dy = D(_rand_act(N, Pq, Qq, K, 15))
+    w = (torch.randn(K, R, R, C, generator=torch.Generator().manual_seed(16)) * 0.05).float()
+    _, wt = pack(w.to(DEV), C, R * R * C)
+    add = D(_rand_act(N, H, W, C, 17))
+    outs = []
+    try:
+        for one in (1, 0):
+            call("avt_set_s2_dgrad_one", one)
+            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+            dxa = torch.empty_like(dx)
+            dxi = add.clone()
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dxa), P(add), N, H, W, C, K, R, R, st, pad, S())
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dxi), P(dxi), N, H, W, C, K, R, R, st, pad, S())
+            torch.cuda.synchronize()
+            outs.append((dx, dxa, dxi))
+    finally:
+        call("avt_set_s2_dgrad_one", 1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = torch.nn.grad.conv2d_input((N, C, H, W), w.to(DEV).to(torch.bfloat16).double().permute(0, 3, 1, 2),
+                                     dy.double().permute(0, 3, 1, 2), stride=st, padding=pad).permute(0, 2, 3, 1)
+    assert rel_err(outs[0][0], ref) < 8e-3
+    assert rel_err(outs[0][1], ref + add.double()) < 8e-3
+
+
 def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
     wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, cp, creal, K, R, R, st, pad)) if slab else 0
     ws = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
