@@ -12,6 +12,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
 bash tools/pmc_traffic.sh > gpurun_out/traffic.log 2>&1; rc=$?; echo "traffic rc=$rc"; head -4 gpurun_out/traffic/summary.txt; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --batch 32 --steps 20 --no-cpu-baseline > gpurun_out/bench_b32.log 2>&1; rc=$?; echo "b32 rc=$rc"; tail -1 gpurun_out/bench_b32.log | cut -c1-200
 [ $rc -ne 0 ] && exit $rc
+rm -rf gpurun_out/prof32
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof32" -o run -- python "$R/bench.py" --batch 32 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof32.log 2>&1; rc=$?; echo "prof32 rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --workload tube --no-cpu-baseline > gpurun_out/bench_tube.log 2>&1; rc=$?; echo "tube rc=$rc"; tail -1 gpurun_out/bench_tube.log | cut -c1-120; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --workload twoview --no-cpu-baseline > gpurun_out/bench_twoview.log 2>&1; rc=$?; echo "twoview rc=$rc"; tail -1 gpurun_out/bench_twoview.log | cut -c1-120
 exit $rc
