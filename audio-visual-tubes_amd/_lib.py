@@ -47,6 +47,7 @@ SIGNATURES = {
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
+    "avt_set_halo_stages": (_I, [_I, _I]),
     "avt_set_c64": (_I, [_I]),
     "avt_set_s2_dgrad_one": (_I, [_I]),
     "avt_set_stem_kernel": (_I, [_I]),
@@ -90,6 +91,8 @@ SIGNATURES = {
                              _P]),
     "avt_hardway_bwd_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                 _P, _P, _I, _P]),
+    "avt_hardway_attention_fwd": (_I, [_P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "avt_hardway_attention_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
     "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "avt_npratio_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),

@@ -59,6 +59,8 @@ def flat_adam_state_dict(model: torch.nn.Module, opt) -> dict:
     group = {"lr": opt.lr, "betas": tuple(opt.betas), "eps": opt.eps, "weight_decay": opt.wd, "amsgrad": False,
              "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
              "params": list(range(len(names)))}
+    if getattr(opt, "initial_lr", None) is not None:  # what torch's schedulers add to the group
+        group["initial_lr"] = opt.initial_lr
     return {"state": state, "param_groups": [group]}
 
 
@@ -73,6 +75,7 @@ def load_flat_adam_state_dict(model: torch.nn.Module, opt, sd: dict) -> None:
     if len(g["params"]) != len(names):
         raise ValueError(f"avt: optimizer state covers {len(g['params'])} parameters, model has {len(names)}")
     opt.lr, opt.betas, opt.eps, opt.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+    opt.initial_lr = g.get("initial_lr")
     steps = set()
     with torch.no_grad():
         opt.exp_avg.zero_()

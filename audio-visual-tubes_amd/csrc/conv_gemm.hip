@@ -537,6 +537,17 @@ static int halo_enabled() {
   }
   return g_halo;
 }
+// weight-ring stages of the layer3/4 halo tiles (A/B knobs): AVT_HALO_NST for the 128 x 128 tile (2: two
+// blocks per CU; 3: one), AVT_HALO_SMALL_NST for the 64 x 128 small-batch tile (2..5)
+static int g_halo_nst = -1, g_halo_small_nst = -1;  // -1: from the environment (default 2); avt_set_halo_stages
+static int halo_nst() {
+  if (g_halo_nst < 0) g_halo_nst = getenv("AVT_HALO_NST") ? atoi(getenv("AVT_HALO_NST")) : 2;
+  return g_halo_nst;
+}
+static int halo_small_nst() {
+  if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 2;
+  return g_halo_small_nst;
+}
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
 static int c64_enabled() {
   if (g_c64 < 0) {
@@ -585,6 +596,13 @@ extern "C" int avt_set_s2_dgrad_one(int on) {
 
 extern "C" int avt_set_halo(int on) {
   avt::g_halo = on < 0 ? 0 : (on > 2 ? 2 : on);
+  return AVT_OK;
+}
+
+extern "C" int avt_set_halo_stages(int nst128, int nst64) {
+  AVT_REQUIRE(nst128 >= 2 && nst128 <= 3 && nst64 >= 2 && nst64 <= 5, "set_halo_stages: nst128 in 2..3, nst64 in 2..5");
+  avt::g_halo_nst = nst128;
+  avt::g_halo_small_nst = nst64;
   return AVT_OK;
 }
 
@@ -885,8 +903,14 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
   if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && g_nt64_config == 1 &&
       p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
     if (p.Ng % 128 == 0) {
-      if (halo_eligible(p) && 64 + 2 * p.OW + 2 <= 104)
-        launch_halo<MODE, 2, 2, 1, 2, 2, 104>(p, st);  // 64 x 128 halo tile
+      if (halo_eligible(p) && 64 + 2 * p.OW + 2 <= 104) {  // 64 x 128 halo tile
+        switch (halo_small_nst()) {
+          case 3: launch_halo<MODE, 2, 2, 1, 2, 3, 104>(p, st); break;
+          case 4: launch_halo<MODE, 2, 2, 1, 2, 4, 104>(p, st); break;
+          case 5: launch_halo<MODE, 2, 2, 1, 2, 5, 104>(p, st); break;
+          default: launch_halo<MODE, 2, 2, 1, 2, 2, 104>(p, st); break;
+        }
+      }
       else
         launch_glds<MODE, 2, 2, 1, 2, 3>(p, st);  // 64 x 128, k32, 3 stages
     } else {
@@ -906,6 +930,8 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
     }
     else if (g_halo == 2)
       launch_halo<MODE, 4, 2, 2, 1>(p, st);  // 256 x 64, 8 waves (A/B only)
+    else if (halo_nst() == 3)
+      launch_halo<MODE, 2, 2, 2, 2, 3, 168>(p, st);  // 128 x 128, 3 weight stages: 96 KB LDS, 1 block per CU
     else
       launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st);  // 128 x 128, 4 waves, 80 KB LDS: 2 blocks per CU
     return;

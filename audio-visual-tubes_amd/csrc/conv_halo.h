@@ -27,15 +27,22 @@ struct HaloArgs {
 // WM x WN waves, each TM x TN 32x32 accumulators: BM = WM*TM*32 rows, BN = WN*TN*32 columns.
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
 // EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
+// LDS of the main loop (two patch buffers + the weight ring): two blocks per CU when two fit in 160 KB
+template <int WN, int TN, int NSTB, int PRMAX>
+constexpr int halo_blocks_per_cu() {
+  return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
+}
+
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false>
-__global__ __launch_bounds__(WM * WN * 64, 2) void conv_halo_kernel(GemmNTParams p, HaloArgs ha) {
+__global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
+    GemmNTParams p, HaloArgs ha) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int BK = 64, RB = 128, RPI = 8;  // 64 channels = one 128-B row; 8 rows per 1 KiB DMA
   constexpr int BR = BN / (NW * RPI);        // weight-tile DMA instructions per wave per step
   static_assert(BR >= 1 && BR * NW * RPI == BN, "weight tile / wave split");
   constexpr int PINSTR = (PRMAX + RPI - 1) / RPI;  // DMA instructions per patch
-  static_assert(NSTB == 2 || NSTB == 3, "NSTB");
+  static_assert(NSTB >= 2 && NSTB <= 5, "NSTB");
   constexpr int NPIECE = 10 - NSTB;  // patch pieces ride on taps NSTB-1 .. 8
   constexpr int AP = (PINSTR + NPIECE * NW - 1) / (NPIECE * NW);  // patch instructions per wave per piece
   constexpr int ABUF = PRMAX * RB + 1024;  // a patch buffer + 8 zero rows (masked taps read them)
@@ -170,16 +177,24 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_halo_kernel(GemmNTParams
     for (int t = 0; t < 9; ++t) {
       {
         // step s = c*9 + t: its stage is s % NSTB -- (c + t) % 2 for NSTB 2 (9 odd), t % 3 for 3
-        const int stage = NSTB == 2 ? (c + t) & 1 : t % 3;
-        // step s has landed once only step s+1's loads may be outstanding (issued after it)
+        const int stage = NSTB == 2 ? (c + t) & 1 : NSTB == 3 ? t % 3 : (c * 9 + t) % NSTB;
+        // step s has landed once only steps s+1 .. s+NSTB-2 may be outstanding (issued after it): BR weight
+        // loads each, + AP patch loads for those with a tap >= NSTB-1 (t is a constant after unrolling)
         if constexpr (NSTB == 2) {
           wait_vmcnt<0>();
         } else {
-          const int tn = t + 1 == 9 ? 0 : t + 1;
-          if (tn >= NSTB - 1)
-            wait_vmcnt<BR + AP>();
+          int pieces = 0;
+#pragma unroll
+          for (int j = 1; j <= NSTB - 2; ++j) pieces += ((t + j) % 9 >= NSTB - 1) ? 1 : 0;
+          constexpr int W0 = (NSTB - 2) * BR;
+          if (pieces == 0)
+            wait_vmcnt<W0>();
+          else if (pieces == 1)
+            wait_vmcnt<W0 + AP>();
+          else if (pieces == 2)
+            wait_vmcnt<W0 + 2 * AP>();
           else
-            wait_vmcnt<BR>();
+            wait_vmcnt<W0 + 3 * AP>();
         }
         __builtin_amdgcn_s_barrier();
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
@@ -194,7 +209,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void conv_halo_kernel(GemmNTParams
         {  // the ring stage read at step s-1; every wave has passed that
           const int tn = t + NSTB - 1 >= 9 ? t + NSTB - 1 - 9 : t + NSTB - 1;
           const int cn = t + NSTB - 1 >= 9 ? c + 1 : c;
-          const int stn = NSTB == 2 ? (stage ^ 1) : (stage + 2) % 3;
+          const int stn = NSTB == 2 ? (stage ^ 1) : (stage + NSTB - 1) % NSTB;
           issue(cn, tn, stn);
         }
 #pragma unroll

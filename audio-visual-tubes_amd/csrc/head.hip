@@ -9,27 +9,56 @@
 
 namespace avt {
 
+// 8 consecutive elements of a bf16 or fp32 row as fp32
+__device__ __forceinline__ void load8f(const bf16_t* p, float* o) {
+  const u32x4 q = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o[2 * e] = bf2f((bf16_t)(q[e] & 0xffff));
+    o[2 * e + 1] = bf2f((bf16_t)(q[e] >> 16));
+  }
+}
+__device__ __forceinline__ void load8f(const float* p, float* o) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    o[e] = a[e];
+    o[4 + e] = b[e];
+  }
+}
+__device__ __forceinline__ void store8f(bf16_t* p, const float* x) {
+  u32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = pack2(x[2 * e], x[2 * e + 1]);
+  *reinterpret_cast<u32x4*>(p) = o;
+}
+__device__ __forceinline__ void store8f(float* p, const float* x) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{x[0], x[1], x[2], x[3]};
+  *reinterpret_cast<f32x4*>(p + 4) = f32x4{x[4], x[5], x[6], x[7]};
+}
+
 // ---- per-(b,p) norms of the vision map: one wave per row of C channels ----
-__global__ __launch_bounds__(256) void vis_norm_kernel(const bf16_t* __restrict__ v, float* __restrict__ inv,
+// NORM = false (HardWayAttention, model.py:46-60, which takes the features as given): inv = 1.
+template <typename T, bool NORM>
+__global__ __launch_bounds__(256) void vis_norm_kernel(const T* __restrict__ v, float* __restrict__ inv,
                                                        float* __restrict__ vsum, int rows, int C) {
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
   if (w >= rows) return;
-  const bf16_t* src = v + (size_t)w * C;
+  const T* src = v + (size_t)w * C;
   float ss = 0.f, s = 0.f;
   for (int c = lane * 8; c < C; c += 512) {
-    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
-    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
+    float x[8];
+    load8f(src + c, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = bf2f(u[e] & 0xffff), b = bf2f(u[e] >> 16);
-      ss += a * a + b * b;
-      s += a + b;
+    for (int e = 0; e < 8; ++e) {
+      ss += x[e] * x[e];
+      s += x[e];
     }
   }
   ss = wave_sum(ss);
   s = wave_sum(s);
   if (lane == 0) {
-    inv[w] = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    inv[w] = NORM ? 1.f / fmaxf(sqrtf(ss), 1e-12f) : 1.f;
     vsum[w] = s;
   }
 }
@@ -360,36 +389,33 @@ __global__ __launch_bounds__(256) void hardway_logits_bwd_kernel(const float* __
 
 // ---- normalize backward for the vision map: gv = inv*(dvh - vh*<vh,dvh>), vh = v*inv ----
 // dm (optional) [rows]: gradient w.r.t. mean_c(vh) (weighted_A path) — adds dm/C to every channel of dvh.
-__global__ __launch_bounds__(256) void vis_norm_bwd_kernel(const bf16_t* __restrict__ v, const float* __restrict__ inv,
+// NORM = false (no normalisation in the forward): gv = dvh (+ dm/C).
+template <typename T, bool NORM>
+__global__ __launch_bounds__(256) void vis_norm_bwd_kernel(const T* __restrict__ v, const float* __restrict__ inv,
                                                            const float* __restrict__ dvh, const float* __restrict__ dm,
-                                                           bf16_t* __restrict__ gv, int rows, int C) {
+                                                           T* __restrict__ gv, int rows, int C) {
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
   if (w >= rows) return;
-  const bf16_t* src = v + (size_t)w * C;
+  const T* src = v + (size_t)w * C;
   const float* d = dvh + (size_t)w * C;
   const float iv = inv[w];
   const float dmc = dm ? dm[w] / (float)C : 0.f;
   float dot = 0.f;
-  for (int c = lane * 8; c < C; c += 512) {
-    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
-    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
+  if (NORM) {
+    for (int c = lane * 8; c < C; c += 512) {
+      float x[8];
+      load8f(src + c, x);
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      dot += bf2f(u[e] & 0xffff) * (d[c + 2 * e] + dmc) + bf2f(u[e] >> 16) * (d[c + 2 * e + 1] + dmc);
-  }
-  dot = wave_sum(dot) * iv;  // <vh, dvh>
-  for (int c = lane * 8; c < C; c += 512) {
-    const u32x4 q = *reinterpret_cast<const u32x4*>(src + c);
-    const unsigned* u = reinterpret_cast<const unsigned*>(&q);
-    u32x4 o;
-    unsigned* ou = reinterpret_cast<unsigned*>(&o);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = iv * (d[c + 2 * e] + dmc - bf2f(u[e] & 0xffff) * iv * dot);
-      const float b = iv * (d[c + 2 * e + 1] + dmc - bf2f(u[e] >> 16) * iv * dot);
-      ou[e] = pack2(a, b);
+      for (int e = 0; e < 8; ++e) dot += x[e] * (d[c + e] + dmc);
     }
-    *reinterpret_cast<u32x4*>(gv + (size_t)w * C + c) = o;
+    dot = wave_sum(dot) * iv;  // <vh, dvh>
+  }
+  for (int c = lane * 8; c < C; c += 512) {
+    float x[8], o[8];
+    if (NORM) load8f(src + c, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = NORM ? iv * (d[c + e] + dmc - x[e] * iv * dot) : d[c + e] + dmc;
+    store8f(gv + (size_t)w * C + c, o);
   }
 }
 
@@ -623,7 +649,8 @@ extern "C" int avt_hardway_fwd(const void* v, const float* an, int B, int P, int
   AVT_REQUIRE(C % 8 == 0 && B >= 1 && P >= 1, "hardway_fwd: bad shape B=%d P=%d C=%d", B, P, C);
   hipStream_t st = (hipStream_t)stream;
   const int rows = B * P;
-  hipLaunchKernelGGL(vis_norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, vsum, rows, C);
+  hipLaunchKernelGGL((vis_norm_kernel<bf16_t, true>), dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv,
+                     vsum, rows, C);
   // A0[(i,p)][j] = inv[(i,p)] * sum_c v[(i,p)][c] * an[j][c]
   sgemm<bf16_t, float>(rows, B, C, (const bf16_t*)v, C, 1, an, 1, C, inv, nullptr, A0, B, 1, st);
   hipLaunchKernelGGL(hardway_logits_kernel, dim3(B), dim3(1024), 0, st, A0, vsum, inv, B, P, C, eps1, eps2, tau,
@@ -677,8 +704,8 @@ extern "C" int avt_hardway_bwd_ex(const void* v, const float* an, const float* i
   if (splits > 64) splits = 64;
   sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st, 1);
   if (gv != nullptr)
-    hipLaunchKernelGGL(vis_norm_bwd_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v, inv, dvh,
-                       dwA != nullptr ? dm : nullptr, (bf16_t*)gv, rows, C);
+    hipLaunchKernelGGL((vis_norm_bwd_kernel<bf16_t, true>), dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v,
+                       inv, dvh, dwA != nullptr ? dm : nullptr, (bf16_t*)gv, rows, C);
   return check_launch("hardway_bwd");
 }
 
@@ -688,6 +715,54 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
                                void* gv, float* gan, int gan_accumulate, void* stream) {
   return avt_hardway_bwd_ex(v, an, inv, A0, save, dlogits, B, P, C, eps1, eps2, tau, trimap, use_neg, dwA, vsum, dm,
                             nullptr, nullptr, nullptr, dA0, dvh, gv, gan, gan_accumulate, stream);
+}
+
+// Standalone HardWayAttention (model.py:38-60): the head on fp32 features taken as given (no
+// normalisation inside; FullModel normalises before the call), trimap and Neg on, fp32 throughout.
+//   v [B][P][C] fp32 ('(b t) (h w) c' of video_features), an [B][C] fp32 (audio_features)
+//   outputs: logits [B][B+2], A [B][P] (+ Pos/Neg/wA [B][P], scratch of the shared logits kernel)
+//   saved for backward: inv [B][P] (= 1), vsum [B][P], A0 [B][P][B], save [B][2B+4]
+extern "C" int avt_hardway_attention_fwd(const float* v, const float* an, int B, int P, int C, float eps1, float eps2,
+                                         float tau, float* inv, float* vsum, float* A0, float* save, float* logits,
+                                         float* Aout, float* Pos, float* Neg, float* wA, void* stream) {
+  AVT_REQUIRE(v && an && inv && vsum && A0 && save && logits && Aout && Pos && Neg && wA,
+              "hardway_attention_fwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && B >= 1 && P >= 1, "hardway_attention_fwd: bad shape B=%d P=%d C=%d", B, P, C);
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = B * P;
+  hipLaunchKernelGGL((vis_norm_kernel<float, false>), dim3((rows + 3) / 4), dim3(256), 0, st, v, inv, vsum, rows, C);
+  sgemm<float, float>(rows, B, C, v, C, 1, an, 1, C, nullptr, nullptr, A0, B, 1, st);
+  hipLaunchKernelGGL(hardway_logits_kernel, dim3(B), dim3(1024), 0, st, A0, vsum, inv, B, P, C, eps1, eps2, tau, 1, 1,
+                     logits, Aout, Pos, Neg, wA, save);
+  return check_launch("hardway_attention_fwd");
+}
+
+// Backward of avt_hardway_attention_fwd from d logits (and optionally d A): gv [B][P][C] fp32 (d video
+// features; dvh [B][P][C] fp32 and dA0 [B][P][B] are workspace), gan [B][C] fp32 (d audio features).
+extern "C" int avt_hardway_attention_bwd(const float* v, const float* an, const float* inv, const float* A0,
+                                         const float* save, const float* dlogits, const float* gA, int B, int P,
+                                         int C, float eps1, float eps2, float tau, float* dA0, float* dvh, float* gv,
+                                         float* gan, void* stream) {
+  AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && dvh && gv && gan,
+              "hardway_attention_bwd: null pointer");
+  AVT_REQUIRE(C % 8 == 0 && B >= 1 && P >= 1, "hardway_attention_bwd: bad shape B=%d P=%d C=%d", B, P, C);
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = B * P;
+  const int nslice = (int)min(64LL, max(1LL, ((long long)P * B + 2047) / 2048));
+  hipLaunchKernelGGL(hardway_logits_bwd_kernel, dim3(B, nslice), dim3(256), 0, st, A0, save, dlogits, B, P, eps1, eps2,
+                     tau, 1, 1, dA0);
+  if (gA != nullptr)
+    hipLaunchKernelGGL(hardway_aux_bwd_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, A0, gA, nullptr, nullptr,
+                       B, P, eps1, eps2, tau, 1, dA0);
+  sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, gan, B * C);
+  int splits = rows / 256;
+  if (splits < 1) splits = 1;
+  if (splits > 64) splits = 64;
+  sgemm<float, float>(B, C, rows, dA0, 1, B, v, C, 1, nullptr, nullptr, gan, C, splits, st, 1);
+  hipLaunchKernelGGL((vis_norm_bwd_kernel<float, false>), dim3((rows + 3) / 4), dim3(256), 0, st, v, inv, dvh,
+                     nullptr, gv, rows, C);
+  return check_launch("hardway_attention_bwd");
 }
 
 // The 16-frame two-view loss combination (train_hardway.py:134-142) from the two CE values.

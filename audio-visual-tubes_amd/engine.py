@@ -17,7 +17,12 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 from ._lib import call, query
-from .trunk import P, Store, Trunk, stream_ptr
+from .trunk import P, Store, Trunk, drive, stream_ptr
+
+# A/B knob: AVT_INTERLEAVE=0 issues the side branch's launches before the main branch's (round-2 order)
+_INTERLEAVE = os.environ.get("AVT_INTERLEAVE", "1") != "0"
+# >0: branch step k waits for the other branch's step k - LOCKSTEP (cross-stream edges in the graph)
+_LOCKSTEP = int(os.environ.get("AVT_LOCKSTEP", "0"))
 
 # ---------------------------------------------------------------------------------------------
 # parameter inventory (state_dict of the reference AVENet, model.py:89-110 + base_models.py:113-169)
@@ -89,6 +94,25 @@ class FlatStore:
                     self.nbt[self.nbt_names.index(n)] = b.detach().long()
         self.rebind()
 
+    def mirror(self, device) -> "FlatStore":
+        """A store with this one's layout on another device, bound to no module (the per-GPU weights of
+        an nn.DataParallel replica; refresh with sync_from)."""
+        m = FlatStore.__new__(FlatStore)
+        m.module = None
+        m.trainable, m.pnames, m.n_train = self.trainable, self.pnames, self.n_train
+        m.poff, m.boff, m.nbt_names = self.poff, self.boff, self.nbt_names
+        m.flat = torch.empty_like(self.flat, device=device)
+        m.bflat = torch.empty_like(self.bflat, device=device)
+        m.nbt = torch.empty_like(self.nbt, device=device)
+        m.sync_from(self)
+        return m
+
+    def sync_from(self, src: "FlatStore"):
+        """Copy src's parameters, float buffers and counters (same layout) into this store."""
+        self.flat.copy_(src.flat)
+        self.bflat.copy_(src.bflat)
+        self.nbt.copy_(src.nbt)
+
     def raw(self, name: str) -> torch.Tensor:
         """fp32 storage of a parameter: conv weights as [K][R][S][C] (OHWI), others as-is."""
         off, shape = self.poff[name]
@@ -128,6 +152,8 @@ class FlatStore:
             mods[mname]._buffers[bname] = self.nbt[i]
 
     def apply(self, fn):
+        if self.module is None:
+            raise RuntimeError("avt: a mirrored FlatStore is not bound to a module")
         self.flat = fn(self.flat)
         self.bflat = fn(self.bflat)
         self.nbt = fn(self.nbt)
@@ -216,6 +242,41 @@ class AVEngine:
         if self.concurrent and enabled and self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)
 
+    def _interleave(self, side_gen, main_gen):
+        """Issue two launch generators (Trunk.*_iter) alternately, side_gen's launches on the side
+        stream, main_gen's on the current one, forked before and joined after; returns both values.
+
+        The issue order is what a HIP graph replays: its nodes are dispatched in capture order, and a
+        branch captured after the other one starts only when the dispatcher reaches it (measured at
+        B=32: the vision forward started 0.7 ms into the step, after the whole audio forward had been
+        dispatched, and the two backward branches ran one after the other).  Interleaved issue keeps
+        both queues fed.  Not concurrent: side_gen then main_gen on the current stream."""
+        if not self.concurrent:
+            return drive(side_gen), drive(main_gen)
+        side = self._side_stream()
+        main = torch.cuda.current_stream()
+        side.wait_stream(main)
+        res, live = [None, None], [True, True]
+        evs = [[], []]  # per branch: an event after each of its launch groups (lockstep edges)
+        while live[0] or live[1]:
+            for i, (gen, st) in enumerate(((side_gen, side), (main_gen, main))):
+                if not live[i] or (i == 1 and live[0] and not _INTERLEAVE):
+                    continue
+                with torch.cuda.stream(st):
+                    k = len(evs[i])
+                    if _LOCKSTEP and live[1 - i] and k >= _LOCKSTEP and len(evs[1 - i]) > k - _LOCKSTEP:
+                        st.wait_event(evs[1 - i][k - _LOCKSTEP])
+                    try:
+                        next(gen)
+                    except StopIteration as e:
+                        live[i], res[i] = False, e.value
+                    if _LOCKSTEP:
+                        ev = torch.cuda.Event()
+                        ev.record(st)
+                        evs[i].append(ev)
+        main.wait_stream(side)
+        return res[0], res[1]
+
     def _setup_trunks(self):
         self.img = Trunk("imgnet.", "vision")
         self.aud = Trunk("audnet.", "audio")
@@ -294,7 +355,7 @@ class AVEngine:
 
         def audio_branch():
             xa = self._to_nhwc(audio, 1)
-            a, tape_a = self.aud.forward(xa, self.store, training, io_a)
+            a, tape_a = yield from self.aud.forward_iter(xa, self.store, training, io_a)
             C = a.shape[-1]
             an = torch.empty(B, C, device=dev, dtype=torch.float32)
             amax = torch.empty(B, C, device=dev, dtype=torch.int32)
@@ -303,15 +364,12 @@ class AVEngine:
                  stream_ptr())
             return a, tape_a, an, amax, anorm
 
-        if self.concurrent:
-            with self._branch():  # audio trunk (side stream) || vision trunk (current stream)
-                a, tape_a, an, amax, anorm = audio_branch()
-        xi = self._to_nhwc(image, 4)
-        v, tape_i = self.img.forward(xi, self.store, training, io_v)
-        if self.concurrent:
-            self._join()
-        else:
-            a, tape_a, an, amax, anorm = audio_branch()
+        def vision_branch():
+            xi = self._to_nhwc(image, 4)
+            return (yield from self.img.forward_iter(xi, self.store, training, io_v))
+
+        # audio trunk (side stream) || vision trunk (current stream), launches interleaved
+        (a, tape_a, an, amax, anorm), (v, tape_i) = self._interleave(audio_branch(), vision_branch())
         _, h, w, C = v.shape
         Pn = h * w
         L = B + (2 if self.neg else 1)
@@ -407,27 +465,31 @@ class AVEngine:
         self.store.grads = self.flat.grad_views(gflat)
         hi = self.img.HI_BLOCK
         seg = on_boundary is not None  # two segments (joined at the boundary) only when someone listens
+        aud, img, ta, ti = self.aud, self.img, tape["aud"], tape["img"]
+
+        def audio_hi():
+            ga = torch.empty_like(a)
+            call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
+                 a.shape[1] * a.shape[2], C, stream_ptr())
+            return (yield from aud.backward_blocks_iter(ta, ga, self.store, hi, len(aud.blocks)))
+
+        def lo(tr, tp, g, pm):
+            g, _ = yield from tr.backward_blocks_iter(tp, g, self.store, 0, hi, pm)
+            yield from tr.backward_stem_iter(tp, g, self.store)
+
+        def chain(tr, tp, first):
+            g, pm = yield from first
+            yield from lo(tr, tp, g, pm)
+
         try:
-            with self._branch():  # audio backward (side stream) || vision backward
-                ga = torch.empty_like(a)
-                call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
-                     a.shape[1] * a.shape[2], C, stream_ptr())
-                ga, pa = self.aud.backward_blocks(tape["aud"], ga, self.store, hi, len(self.aud.blocks))
-                if not seg:
-                    ga, _ = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi, pa)
-                    self.aud.backward_stem(tape["aud"], ga, self.store)
-            gv, pv = self.img.backward_blocks(tape["img"], gv, self.store, hi, len(self.img.blocks))
-            if seg:
-                self._join()
-                on_boundary((self.img.prefix + "hi", self.aud.prefix + "hi"))
-                with self._branch():  # second segment
-                    ga, _ = self.aud.backward_blocks(tape["aud"], ga, self.store, 0, hi, pa)
-                    self.aud.backward_stem(tape["aud"], ga, self.store)
-            gv, _ = self.img.backward_blocks(tape["img"], gv, self.store, 0, hi, pv)
-            self.img.backward_stem(tape["img"], gv, self.store)
-            self._join()
-            if seg:
-                on_boundary((self.img.prefix + "lo", self.aud.prefix + "lo"))
+            img_hi = img.backward_blocks_iter(ti, gv, self.store, hi, len(img.blocks))
+            if seg:  # segment 1: layer4+layer3 of both trunks; boundary; segment 2: the rest
+                (ga, pa), (gv, pv) = self._interleave(audio_hi(), img_hi)
+                on_boundary((img.prefix + "hi", aud.prefix + "hi"))
+                self._interleave(lo(aud, ta, ga, pa), lo(img, ti, gv, pv))
+                on_boundary((img.prefix + "lo", aud.prefix + "lo"))
+            else:
+                self._interleave(chain(aud, ta, audio_hi()), chain(img, ti, img_hi))
         finally:
             self.store.grads = None
 

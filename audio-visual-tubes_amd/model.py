@@ -114,6 +114,8 @@ class ResNet(nn.Module):
             parent, prefix = self._avt_parent[0](), self._avt_parent[1]
             if parent is None:
                 raise RuntimeError("avt: the AVENet owning this trunk no longer exists")
+            if getattr(parent, prefix.rstrip("."), None) is not self:
+                raise RuntimeError("avt: this trunk is no longer its parent's (a copied trunk; copy the whole model)")
             flat = parent._flat
         else:
             parent, prefix, flat = self, "", self._flat_store()
@@ -270,22 +272,41 @@ class AVENet(nn.Module):
                 nn.init.normal_(m.weight, mean=1, std=0.02)
                 nn.init.constant_(m.bias, 0)
         self._flat = FlatStore(self)
-        self._engine: Optional[AVEngine] = None
+        # engines by device index: the model's own (over self._flat) and, for nn.DataParallel replicas on
+        # other GPUs, one over a mirror of the flat store there.  A dict, so that replicas (which get a
+        # shallow copy of this __dict__) create and find them in the model's cache.
+        self._engines = {}
+        for prefix, net in (("imgnet.", self.imgnet), ("audnet.", self.audnet)):
+            net._adopt(self, prefix)
+
+    def __setstate__(self, state):
+        """copy.deepcopy / unpickling: the trunks must point at this copy's flat store, not the original's
+        (their parent link is a weakref, which deepcopy shares); engines are rebuilt lazily."""
+        super().__setstate__(state)
+        self._flat.module = self
+        self._flat.rebind()  # deepcopy clones each Parameter on its own: make them views of the copied store again
+        self._engines = {}
         for prefix, net in (("imgnet.", self.imgnet), ("audnet.", self.audnet)):
             net._adopt(self, prefix)
 
     # -- storage management: keep the flat buffers when moved (.cuda(), .to(dev)) --
     def _apply(self, fn, recurse=True):
         self._flat.apply(fn)
-        self._engine = None
+        self._engines.clear()
         for net in (self.imgnet, self.audnet):
             net._avt_engine = None
         return self
 
-    def engine(self) -> AVEngine:
-        if self._engine is None:
-            self._engine = AVEngine(self._flat, self.epsilon, self.epsilon2, self.tau, self.trimap, self.Neg)
-        e = self._engine
+    def engine(self, device: Optional[torch.device] = None) -> AVEngine:
+        """The engine on `device` (default: where the flat store lives)."""
+        own = self._flat.flat.device
+        dev = own if device is None else torch.device(device)
+        key = dev.index if dev.type == "cuda" else -1
+        e = self._engines.get(key)
+        if e is None:
+            flat = self._flat if dev == own else self._flat.mirror(dev)
+            e = self._engines.setdefault(key, AVEngine(flat, self.epsilon, self.epsilon2, self.tau, self.trimap,
+                                                       self.Neg))
         e.epsilon, e.epsilon2, e.tau, e.tri_map, e.neg = self.epsilon, self.epsilon2, self.tau, self.trimap, self.Neg
         return e
 
@@ -293,7 +314,44 @@ class AVENet(nn.Module):
         mods = dict(self.named_parameters())
         return [mods[n] for n in self._flat.pnames]
 
+    def _replica_forward(self, image, audio):
+        """Forward of an ``nn.DataParallel(model)`` replica (train_hardway_1frame.py:93 and every entry
+        script).  torch's replicate() gives each replica a shallow copy of this module's __dict__, an
+        empty _parameters and the broadcast copies of the parameters as plain attributes (on its GPU).
+        The replica on the model's own GPU runs the model's engine, so its BN running statistics are the
+        module's buffers (DataParallel keeps replica 0's); a replica on another GPU runs an engine over a
+        mirror of the flat store there, refreshed from the model's store on every forward (its running-
+        statistic updates are dropped, as DataParallel drops them).  Each replica contrasts only its own
+        B/G clips, as in the reference.  The broadcast copies are the autograd inputs, so the gradients
+        flow back through replicate()'s Broadcast, which sums them onto the module's parameters."""
+        _check_hooks(self)
+        if self.imgnet.layer4._forward_hooks or self.audnet.layer4._forward_hooks:
+            raise NotImplementedError("avt: forward hooks under nn.DataParallel are not supported")
+        dev = image.device
+        eng = self.engine(dev)
+        if eng.flat is not self._flat:
+            eng.flat.sync_from(self._flat)
+        n_train = sum(1 for n in self._flat.pnames if trainable(n))
+        tensors = [self._replica_tensor(n) for n in self._flat.pnames[:n_train]]
+        if any(t.device != dev for t in tensors):
+            raise RuntimeError("avt: DataParallel replica parameters are not on the replica's device")
+        if torch.is_grad_enabled() and self.training and any(t.requires_grad for t in tensors):
+            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, None, image, audio, *tensors)
+        else:
+            out, _ = eng.forward(image, audio, self.training)
+            A, logits, wA, Pos, Neg = out["A"], out["logits"], out["weighted_A"], out["Pos"], out["Neg"]
+        return A, logits, wA, Pos, Neg
+
+    def _replica_tensor(self, name: str) -> torch.Tensor:
+        obj = self
+        parts = name.split(".")
+        for part in parts[:-1]:
+            obj = getattr(obj, part)
+        return getattr(obj, parts[-1])
+
     def forward(self, image, audio):
+        if getattr(self, "_is_replica", False):
+            return self._replica_forward(image, audio)
         _check_hooks(self)
         hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
                   if m._forward_hooks]
@@ -321,10 +379,64 @@ class AVENet(nn.Module):
 # ---------------------------------------------------------------------------------------------
 
 
+class _HardWayAttentionFunction(torch.autograd.Function):
+    """HardWayAttention.forward (model.py:46-60) on avt_hardway_attention_fwd/_bwd: fp32 features,
+    gradients into both inputs."""
+
+    @staticmethod
+    def forward(ctx, audio_features, video_features, eps1: float, eps2: float, tau: float):
+        from ._lib import call, query
+        from .trunk import P, stream_ptr
+
+        b, C, t, h, w = video_features.shape
+        B, Pn = b * t, h * w
+        dev = video_features.device
+        # 'b c t h w -> (b t) (h w) c' (model.py:49 rearrange, channels innermost for the kernels)
+        v = video_features.detach().float().permute(0, 2, 3, 4, 1).contiguous()
+        an = audio_features.detach().float().contiguous()
+        f32 = dict(device=dev, dtype=torch.float32)
+        inv, vsum = torch.empty(B, Pn, **f32), torch.empty(B, Pn, **f32)
+        A0 = torch.empty(B, Pn, B, **f32)
+        save = torch.empty(int(query("avt_hardway_save_floats", B)), **f32)
+        logits = torch.empty(B, B + 2, **f32)
+        A, Pos, Neg = (torch.empty(B, 1, h, w, **f32) for _ in range(3))
+        wA = torch.empty(B, h, w, **f32)
+        call("avt_hardway_attention_fwd", P(v), P(an), B, Pn, C, eps1, eps2, tau, P(inv), P(vsum), P(A0), P(save),
+             P(logits), P(A), P(Pos), P(Neg), P(wA), stream_ptr())
+        ctx.save = (v, an, inv, A0, save)
+        ctx.shape = (b, C, t, h, w)
+        ctx.hp = (eps1, eps2, tau)
+        ctx.dtypes = (audio_features.dtype, video_features.dtype)
+        ctx.set_materialize_grads(False)
+        return A, logits
+
+    @staticmethod
+    def backward(ctx, gA, glogits):
+        from ._lib import call
+        from .trunk import P, stream_ptr
+
+        if gA is None and glogits is None:
+            return None, None, None, None, None
+        v, an, inv, A0, save = ctx.save
+        b, C, t, h, w = ctx.shape
+        B, Pn = b * t, h * w
+        f32 = dict(device=v.device, dtype=torch.float32)
+        dl = torch.zeros(B, B + 2, **f32) if glogits is None else glogits.float().contiguous()
+        ga = None if gA is None else gA.float().contiguous()
+        dA0, dvh, gv = torch.empty(B, Pn, B, **f32), torch.empty(B, Pn, C, **f32), torch.empty(B, Pn, C, **f32)
+        gan = torch.empty(B, C, **f32)
+        eps1, eps2, tau = ctx.hp
+        call("avt_hardway_attention_bwd", P(v), P(an), P(inv), P(A0), P(save), P(dl), P(ga), B, Pn, C, eps1, eps2,
+             tau, P(dA0), P(dvh), P(gv), P(gan), stream_ptr())
+        g_vid = gv.view(b, t, h, w, C).permute(0, 4, 1, 2, 3).to(ctx.dtypes[1])
+        return gan.to(ctx.dtypes[0]), g_vid, None, None, None
+
+
 class HardWayAttention(nn.Module):
-    """model.py:38-60.  Standalone use takes fp32 features (the video map is rounded to bf16 on its
-    way to the head kernel, the precision FullModel's trunk produces it in); inside FullModel the
-    head runs fused on the trunk outputs."""
+    """model.py:38-60: ``forward(audio_features [B,C], video_features [b,C,t,h,w]) -> (A, logits)`` with
+    B = b*t, fp32 throughout, differentiable in both inputs.  Like the reference module it takes the
+    features as given (FullModel normalises them before the call, model.py:31-35); inside FullModel
+    the head runs fused on the trunk outputs instead."""
 
     def __init__(self):
         super().__init__()
@@ -334,29 +446,16 @@ class HardWayAttention(nn.Module):
         self.tau = 0.03
 
     def forward(self, audio_features, video_features):
-        from ._lib import call, query
-        from .trunk import P, stream_ptr
-
         if not video_features.is_cuda or not audio_features.is_cuda:
             raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
+        if video_features.dim() != 5:
+            raise ValueError(f"avt: video_features must be [b,C,t,h,w], got {tuple(video_features.shape)}")
         b, C, t, h, w = video_features.shape
-        B, Pn = b * t, h * w
-        if tuple(audio_features.shape) != (B, C):
-            raise ValueError(f"avt: audio_features must be [{B},{C}], got {tuple(audio_features.shape)}")
-        dev = video_features.device
-        # '(b t) h w c' bf16 — the FullModel trunk's output layout
-        v = video_features.detach().permute(0, 2, 3, 4, 1).contiguous().to(torch.bfloat16)
-        an = audio_features.detach().float().contiguous()
-        f32 = dict(device=dev, dtype=torch.float32)
-        inv, vsum = torch.empty(B, Pn, **f32), torch.empty(B, Pn, **f32)
-        A0 = torch.empty(B, Pn, B, **f32)
-        save = torch.empty(int(query("avt_hardway_save_floats", B)), **f32)
-        logits = torch.empty(B, B + 2, **f32)
-        A, Pos, Neg = (torch.empty(B, 1, h, w, **f32) for _ in range(3))
-        wA = torch.empty(B, h, w, **f32)
-        call("avt_hardway_fwd", P(v), P(an), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, P(inv), P(vsum),
-             P(A0), P(save), P(logits), P(A), P(Pos), P(Neg), P(wA), stream_ptr())
-        return A, logits
+        if tuple(audio_features.shape) != (b * t, C):
+            raise ValueError(f"avt: audio_features must be [{b * t},{C}], got {tuple(audio_features.shape)}")
+        if C % 8 != 0:
+            raise ValueError(f"avt: the channel count must be a multiple of 8 (got {C})")
+        return _HardWayAttentionFunction.apply(audio_features, video_features, self.epsilon, self.epsilon2, self.tau)
 
 
 class _FullModelFunction(torch.autograd.Function):
@@ -402,6 +501,14 @@ class FullModel(nn.Module):
         from .tube import tube_trainable
 
         self._flat = FlatStore(self, tube_trainable)
+        self._engine = None
+        self.audnet._adopt(self, "audnet.")
+
+    def __setstate__(self, state):
+        """copy.deepcopy / unpickling: re-adopt the audio trunk (see AVENet.__setstate__)."""
+        super().__setstate__(state)
+        self._flat.module = self
+        self._flat.rebind()
         self._engine = None
         self.audnet._adopt(self, "audnet.")
 

@@ -6,7 +6,7 @@ Parameters whose ``.grad`` is None are skipped, exactly like torch.
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
 
@@ -74,6 +74,7 @@ class FlatAdam:
         self._coef = torch.zeros(8, device=dev, dtype=torch.float32)  # AVT_ADAM_COEF_FLOATS
         self._host = {"lr": float(lr), "beta1": float(betas[0]), "beta2": float(betas[1]), "eps": float(eps),
                       "wd": float(weight_decay)}
+        self.initial_lr = None  # set by the first scheduler, saved in checkpoints (torch's group 'initial_lr')
         self._hyper = torch.tensor([self._host[k] for k in self._HYPER], device=dev, dtype=torch.float32)
 
     def _set(self, key: str, value: float):
@@ -130,23 +131,42 @@ class FlatAdam:
 class FlatMultiStepLR:
     """torch.optim.lr_scheduler.MultiStepLR (train_hardway_1frame.py:118: milestones [60,100,150,180],
     gamma 0.1, stepped once per epoch at :138) for a FlatAdam: lr = base_lr * gamma^(number of
-    milestones <= epoch).  Writes the device hyper-parameter, so captured step graphs follow."""
+    milestones <= epoch).  Writes the device hyper-parameter, so captured step graphs follow.
 
-    def __init__(self, opt: FlatAdam, milestones, gamma: float = 0.1, last_epoch: int = -1):
+    base_lr is the optimizer's lr for a fresh schedule (last_epoch = -1; recorded as opt.initial_lr,
+    like torch's group 'initial_lr').  Resuming (last_epoch = e >= 0: the constructor's step moves to
+    epoch e+1, as torch's does) takes base_lr from the argument, else opt.initial_lr (restored with the
+    checkpoint), else infers it from the optimizer's current lr -- the restored lr of epoch e+1 -- so
+    the restored lr is kept and the decay never applied twice; later epochs follow the uninterrupted
+    schedule (torch's chainable form multiplies the restored lr at each later milestone: the same)."""
+
+    def __init__(self, opt: FlatAdam, milestones, gamma: float = 0.1, last_epoch: int = -1,
+                 base_lr: Optional[float] = None):
         self.opt = opt
         self.milestones = sorted(int(m) for m in milestones)
         self.gamma = float(gamma)
-        self.base_lr = opt.lr
+        if base_lr is None:
+            if last_epoch == -1:
+                base_lr = opt.lr
+            elif getattr(opt, "initial_lr", None) is not None:
+                base_lr = opt.initial_lr
+            else:
+                base_lr = opt.lr / self.gamma ** self._decays(last_epoch + 1)
+        self.base_lr = float(base_lr)
+        if getattr(opt, "initial_lr", None) is None:
+            opt.initial_lr = self.base_lr
         self.last_epoch = last_epoch
         self.step()
+
+    def _decays(self, epoch: int) -> int:
+        return sum(1 for m in self.milestones if m <= epoch)
 
     def get_last_lr(self):
         return [self.opt.lr]
 
     def step(self):
         self.last_epoch += 1
-        k = sum(1 for m in self.milestones if m <= self.last_epoch)
-        lr = self.base_lr * self.gamma ** k
+        lr = self.base_lr * self.gamma ** self._decays(self.last_epoch)
         if lr != self.opt.lr:
             self.opt.set_lr(lr)
 

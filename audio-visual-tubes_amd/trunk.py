@@ -31,6 +31,15 @@ def stream_ptr():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def drive(gen):
+    """Run a launch generator (Trunk.*_iter) to completion; return its value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
 def conv_out(n: int, k: int, s: int, p: int) -> int:
     return (n + 2 * p - k) // s + 1
 
@@ -214,9 +223,15 @@ class Trunk:
     def forward(self, x: torch.Tensor, store: Store, training: bool, io: Optional[Dict] = None):
         """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape).  io (optional) receives
         "layer4_in": the layer3 output [N,h,w,256] (the input a forward hook on .layer4 sees)."""
+        return drive(self.forward_iter(x, store, training, io))
+
+    def forward_iter(self, x: torch.Tensor, store: Store, training: bool, io: Optional[Dict] = None):
+        """forward() as a generator that yields after each launch group, so that two trunks' launches can
+        be issued interleaved on two streams (engine._interleave); returns forward()'s result."""
         N, H, W, _ = x.shape
         tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
         c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
+        yield
         # bn1 -> relu -> maxpool fused: the full-resolution relu(bn1(c0)) is never stored
         H2, W2 = conv_out(H1, 3, 2, 1), conv_out(W1, 3, 2, 1)
         p0 = torch.empty(N, H2, W2, 64, device=x.device, dtype=torch.bfloat16)
@@ -225,22 +240,27 @@ class Trunk:
         call("avt_stem_bn_relu_maxpool_fwd", P(c0), P(st0[0]), P(st0[1]), P(p0), P(idx), P(carg), N, H1, W1, 64,
              stream_ptr())
         tape.update(c0=c0, st0=st0, idx=idx, carg=carg, H1=H1, W1=W1)
+        yield
         cur, Hc, Wc = p0, H2, W2
         for bi, blk in enumerate(self.blocks):
             if io is not None and bi == 6:
                 io["layer4_in"] = cur
             t = {"x": cur, "H": Hc, "W": Wc}
             c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
+            yield
             h1 = torch.empty_like(c1)
             call("avt_bn_apply", P(c1), P(s1[0]), P(s1[1]), None, None, None, P(h1), N * Ho * Wo, c1.shape[-1], 1,
                  stream_ptr())
+            yield
             c2, s2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training)
+            yield
             out = torch.empty_like(c2)
             # training: the output's ReLU mask as bits ([rows][C/8] u8) for the backward, which then never
             # re-reads `out` (1/16 of its bytes)
             om = torch.empty(c2.numel() // 8, device=x.device, dtype=torch.uint8) if training else None
             if blk["down"] is not None:
                 cd, sd, _, _ = self._conv_bn(cur, N, Hc, Wc, blk["down"], blk["bnd"], store, training)
+                yield
                 res = (P(cd), P(sd[0]), P(sd[1]))
                 t.update(cd=cd, sd=sd)
             else:
@@ -253,6 +273,7 @@ class Trunk:
                      stream_ptr())
             t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, om=om, Ho=Ho, Wo=Wo)
             tape["blocks"].append(t)
+            yield
             cur, Hc, Wc = out, Ho, Wo
         if not training:
             tape = None
@@ -363,6 +384,10 @@ class Trunk:
         return e
 
     def backward_blocks(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int, premasked: bool = False):
+        return drive(self.backward_blocks_iter(tape, g, store, lo, hi, premasked))
+
+    def backward_blocks_iter(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int,
+                             premasked: bool = False):
         """Backward of blocks hi-1 .. lo (BasicBlock.forward, base_models.py:53-69).  Returns (gradient of
         block lo's input, premasked): with premasked the gradient is already multiplied by block lo-1's
         output ReLU mask and that block's bn2 (+ downsample BN) reductions are accumulated -- each dgrad
@@ -389,17 +414,23 @@ class Trunk:
                 else:
                     g_c2, g_cd = self._bn_bwd_mask(g, t["om"], t["c2"], t["s2"], blk["bn2"], store,
                                                    t["cd"], t["sd"], blk["bnd"])
+            yield
             self._wgrad(t["h1"], g_c2, N, Ho, Wo, blk["conv2"], store)
+            yield
             if FUSE_BN_BWD:  # conv2 dgrad with bn1's backward (ReLU mask from its pre-activation) in the epilogue
                 g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store,
                                    epi=self._epi(store, blk["bn1"], t["c1"], t["s1"]))
                 g_c1 = self._bn_bwd_premasked(g_h1, t["c1"], t["s1"], blk["bn1"], store)
             else:
                 g_h1 = self._dgrad(g_c2, N, Ho, Wo, blk["conv2"], store)
+                yield
                 g_c1 = self._bn_relu_bwd(g_h1, t["c1"], t["s1"], blk["bn1"], store)
+            yield
             self._wgrad(t["x"], g_c1, N, Hc, Wc, blk["conv1"], store)
+            yield
             if not identity:
                 self._wgrad(t["x"], g_cd, N, Hc, Wc, blk["down"], store)
+                yield
             epi = None
             if bi > 0 and FUSE_BN_BWD:  # the next block down: its bn2 (+ downsample BN) backward rides on this dgrad
                 pb, pt = self.blocks[bi - 1], tape["blocks"][bi - 1]
@@ -421,10 +452,14 @@ class Trunk:
                 g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True, epi=epi)
             g = g_x
             premasked = epi is not None
+            yield
         return g, premasked
 
     def backward_stem(self, tape: Dict, g: torch.Tensor, store: Store):
         """maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)."""
+        drive(self.backward_stem_iter(tape, g, store))
+
+    def backward_stem_iter(self, tape: Dict, g: torch.Tensor, store: Store):
         N = tape["N"]
         H1, W1 = tape["H1"], tape["W1"]
         c0, st0 = tape["c0"], tape["st0"]
@@ -434,4 +469,5 @@ class Trunk:
              P(st0[2]), P(st0[3]), P(store.param(self.bn1.prefix + ".weight")),
              P(store.grad(self.bn1.prefix + ".weight")), P(store.grad(self.bn1.prefix + ".bias")), P(g_c0), P(ws),
              N, H1, W1, 64, stream_ptr())
+        yield
         self._wgrad(tape["x"], g_c0, N, tape["H"], tape["W"], self.stem, store)

@@ -4,10 +4,13 @@
                     [--no-cpu-baseline]
     (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
 
-Default workload (BASELINE.json configs[1], the headline): per GPU B=128 clips of one 224x224 RGB
+Default workload: N=1 runs BASELINE.json configs[1], the headline: B=128 clips of one 224x224 RGB
 frame + one 257x300 log-spectrogram; ResNet-18 vision + ResNet-18 audio trunks (bf16 MFMA, fp32
-statistics), fp32 hard-way head + CE, backward, Adam (lr 1e-6, wd 1e-4); N GPUs = weak scaling with
-local negatives and one RCCL all-reduce of the 89.4 MB fp32 gradient per step.
+statistics), fp32 hard-way head + CE, backward, Adam (lr 1e-6, wd 1e-4).  N>1 runs configs[2]: a
+global batch of 256 clips sharded over the N GPUs (256/N per GPU, 32 at N=8; strong scaling), local
+negatives per rank as nn.DataParallel gives them, and the 89.4 MB fp32 gradient all-reduced over
+RCCL in buckets overlapped with the backward.  --batch B fixes the per-GPU batch instead (weak
+scaling at B per GPU).
 
 --workload tube (configs[3], train_3D.py): per GPU b=8 clips of 16x224x224 frames + one 257x300
 spectrogram each; R3D-18 forward (detached, as the reference's hook) + audio ResNet-18 fwd/bwd over
@@ -166,7 +169,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["1frame", "tube", "twoview"], default="1frame")
-    ap.add_argument("--batch", type=int, default=0, help="clips per GPU (default 128; tube, twoview: 8)")
+    ap.add_argument("--batch", type=int, default=0, help="clips per GPU (weak scaling; default: 128 at N=1, "
+                    "256/N at N>1 -- configs[2]'s global batch; tube, twoview: 8 per GPU)")
+    ap.add_argument("--global-batch", type=int, default=0, help="clips over all GPUs (strong scaling; 1frame "
+                    "default for N>1: 256, BASELINE configs[2])")
     ap.add_argument("--frames", type=int, default=16, help="tube, twoview: frames per clip")
     ap.add_argument("--twoview-folded", action="store_true", help="twoview: run the audio trunk over the folded "
                     "16x-repeated spectrogram batch once per view (the reference's arithmetic)")
@@ -198,7 +204,16 @@ def main():
 
     tube = args.workload == "tube"
     twoview = args.workload == "twoview"
-    B = args.batch or (8 if (tube or twoview) else 128)
+    strong = False
+    if args.batch:
+        B = args.batch
+    elif args.global_batch or (world > 1 and not (tube or twoview)):
+        G = args.global_batch or 256
+        if G % world:
+            sys.exit(f"bench.py: global batch {G} does not split over {world} GPUs")
+        B, strong = G // world, True
+    else:
+        B = 8 if (tube or twoview) else 128
     torch.manual_seed(0)
     if twoview:
         model = AVENet(HardWayArgs(), False).to(dev).train()
@@ -221,7 +236,9 @@ def main():
     else:
         model = AVENet(HardWayArgs(), False).to(dev).train()
         inputs = synthetic_inputs(B, dev, seed=1000 + rank)
-        workload = "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam"
+        workload = "train_hardway_1frame step: 224x224 RGB + 257x300 spectrogram, fwd+CE+bwd+Adam" + (
+            f"; configs[2]: global batch {B * world} sharded {B}/GPU" if strong else
+            ("; configs[1]" if B == 128 and world == 1 else ""))
     if twoview:
         step = TwoViewTrainStep(model, lr=4e-6, weight_decay=1e-4, dedup_audio=not args.twoview_folded)
     else:
@@ -283,7 +300,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
             "data": DATA,

@@ -71,6 +71,9 @@ int avt_bn_slots(void);
 /* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
+/* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) in 2..3, nst64 (64 x 128
+ * small-batch tile) in 2..5; all settings give bitwise-identical results (A/B knob) */
+int avt_set_halo_stages(int nst128, int nst64);
 /* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
  * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
  * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
@@ -254,6 +257,19 @@ int avt_hardway_bwd_ex(const void* v, const float* an, const float* inv, const f
                        int use_neg, const float* dwA, const float* vsum, float* dm, const float* gA, const float* gPos,
                        const float* gNeg, float* dA0, float* dvh, void* gv, float* gan, int gan_accumulate,
                        void* stream);
+/* Standalone HardWayAttention()(audio_features, video_features) -> (A, logits) (model.py:38-60): fp32
+ * features taken as given (the module does not normalise them; FullModel normalises before the call,
+ * model.py:31-35), tri-map and Neg on.  v [B][P][C] fp32 = '(b t) (h w) c' of video_features,
+ * an [B][C] fp32.  inv/vsum [B][P], A0 [B][P][B], save [B*(2B+4)] are saved for the backward; Pos, Neg,
+ * wA [B][P] are scratch. */
+int avt_hardway_attention_fwd(const float* v, const float* an, int B, int P, int C, float eps1, float eps2, float tau,
+                              float* inv, float* vsum, float* A0, float* save, float* logits, float* Aout, float* Pos,
+                              float* Neg, float* wA, void* stream);
+/* Its backward: dlogits [B][B+2] and gA [B][P] (or NULL) -> gv [B][P][C] fp32 (d video features,
+ * '(b t) (h w) c'), gan [B][C] fp32 (d audio features).  dA0 [B][P][B], dvh [B][P][C] fp32: workspace. */
+int avt_hardway_attention_bwd(const float* v, const float* an, const float* inv, const float* A0, const float* save,
+                              const float* dlogits, const float* gA, int B, int P, int C, float eps1, float eps2,
+                              float tau, float* dA0, float* dvh, float* gv, float* gan, void* stream);
 /* train_hardway.py:134-142 loss combination of the 16-frame two-view step: given the two CE values
  * (avt_hardway_ce outputs; their dlogits use scale loss_weight/2) and weighted_A of both views
  * ([b*t][P], '(b t)' clip-major), out[5] = {combined, hardway, aug, l2, consistency} and

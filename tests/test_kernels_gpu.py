@@ -211,6 +211,39 @@ def test_halo_matches_gather(case):
         torch.testing.assert_close(a1[:, 0], a0[:, 0], rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("case", [(3, 14, 14, 256, 256, 3, 1, 1), (2, 17, 19, 512, 512, 3, 1, 1),
+                                  (2, 5, 6, 256, 512, 3, 1, 1), (5, 14, 14, 512, 512, 3, 1, 1)])
+def test_halo_stages_bitwise_equal(case):
+    """The halo kernels' weight-ring depth (avt_set_halo_stages) changes only the load pipeline: every
+    setting of both tiles (128-row, and 64-row via avt_set_small_tiles(-1)) gives bitwise-equal outputs
+    and BN partial sums."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 51).relu().to(DEV)
+    g = torch.Generator().manual_seed(52)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, R * R * C)
+    dy = _rand_act(N, H, W, K, 53).to(DEV)
+    try:
+        for small in (0, -1):
+            call("avt_set_small_tiles", small)
+            outs = []
+            for nst in ((2, 2), (3, 3), (2, 4), (2, 5)):
+                call("avt_set_halo_stages", *nst)
+                y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+                acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+                call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
+                dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+                call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+                torch.cuda.synchronize()
+                outs.append((y.view(torch.int16).clone(), dx.view(torch.int16).clone(), acc.view(-1, K, 3)[:, :, 0].sum(0)))
+            for o in outs[1:]:
+                assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+                torch.testing.assert_close(o[2], outs[0][2], rtol=1e-9, atol=1e-6)
+    finally:
+        call("avt_set_halo_stages", 2, 2)
+        call("avt_set_small_tiles", 1)
+
+
 @pytest.mark.parametrize("N,H,W", [(3, 56, 56), (2, 65, 75), (21, 56, 56), (1, 7, 95)])
 def test_c64_matches_gather(N, H, W):
     """Layer-1 persistent resident-weight kernel (avt_set_c64) vs the tap-gather kernel: fwd + BN partials,

@@ -300,3 +300,37 @@ def test_tube_train_step_graph_and_loss():
     sd = m_g.state_dict()
     for n in ("vidnet.conv1.weight", "vidnet.layer4.1.conv2.weight"):
         assert torch.equal(sd[n].cpu(), before[n]), n
+
+
+@pytest.mark.parametrize("b,t,hw,C,normalized", [(2, 3, 7, 512, False), (1, 4, 14, 64, True), (3, 2, 5, 128, False)])
+def test_hardway_attention_standalone_autograd(b, t, hw, C, normalized):
+    """Standalone HardWayAttention()(audio_features, video_features) (model.py:38-60): fp32 outputs and
+    gradients into both inputs against the fp64 oracle (autograd through orc.hardway_attention).
+    The module takes the features as given (no normalisation inside), so un-normalised inputs are a case."""
+    from avt_amd.model import HardWayAttention
+
+    g = torch.Generator().manual_seed(b * 100 + t * 10 + hw)
+    vid = torch.randn(b, C, t, hw, hw, generator=g, dtype=torch.float64) * 0.05
+    aud = torch.randn(b * t, C, generator=g, dtype=torch.float64)
+    if normalized:  # FullModel's call (model.py:31-35)
+        vid = F.normalize(vid, dim=1)
+        aud = F.normalize(aud, dim=1)
+    else:
+        aud = F.normalize(aud, dim=1) * 1.3
+    wl = torch.randn(b * t, b * t + 2, generator=g, dtype=torch.float64)
+    wa = torch.randn(b * t, 1, hw, hw, generator=g, dtype=torch.float64)
+
+    vr, ar = vid.clone().requires_grad_(), aud.clone().requires_grad_()
+    A_r, l_r = orc.hardway_attention(ar, vr)
+    ((l_r * wl).sum() + (A_r * wa).sum()).backward()
+
+    vd = vid.float().to(DEV).requires_grad_()
+    ad = aud.float().to(DEV).requires_grad_()
+    A, logits = HardWayAttention()(ad, vd)
+    assert A.dtype == torch.float32 and logits.dtype == torch.float32 and A.requires_grad
+    ((logits * wl.float().to(DEV)).sum() + (A * wa.float().to(DEV)).sum()).backward()
+    # fp32 arithmetic against fp64: the logits carry 1/0.07 and sigmoids of (A - eps)/0.03
+    assert rel_err(A, A_r.detach()) < 1e-5
+    assert rel_err(logits, l_r.detach()) < 2e-4
+    assert rel_err(vd.grad, vr.grad) < 2e-4
+    assert rel_err(ad.grad, ar.grad) < 2e-4

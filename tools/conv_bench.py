@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--wgrad-halo", default="0", help="comma list of avt_set_wgrad_halo values to sweep")
     ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
+    ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -113,6 +114,16 @@ def main():
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
                 tot[(f"dgrad_small{sv}", 1)] = tot.get((f"dgrad_small{sv}", 1), 0) + ms
             call("avt_set_small_tiles", 2)
+        if args.stages and R == 3 and st == 1:
+            for pair in args.stages.split(";"):
+                call("avt_set_halo_stages", *(int(v) for v in pair.split(",")))
+                ms = timeit(lambda: call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad,
+                                         kg, S()))
+                line += f" | nst[{pair}] fwd {flops / ms / 1e9:6.0f}"
+                ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
+                                         pad, S()))
+                line += f" dgrad {flops / ms / 1e9:6.0f}"
+            call("avt_set_halo_stages", 2, 2)
         if (args.nt64 or args.nt128) and args.halo:
             call("avt_set_halo", 0)  # the tap-gather configs on every shape
         if args.nt64 and K == 64 or args.nt64 and C == 64:
