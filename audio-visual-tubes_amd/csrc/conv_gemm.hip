@@ -537,15 +537,17 @@ static int halo_enabled() {
   }
   return g_halo;
 }
-// weight-ring stages of the layer3/4 halo tiles (A/B knobs): AVT_HALO_NST for the 128 x 128 tile (2: two
-// blocks per CU; 3: one), AVT_HALO_SMALL_NST for the 64 x 128 small-batch tile (2..5)
-static int g_halo_nst = -1, g_halo_small_nst = -1;  // -1: from the environment (default 2); avt_set_halo_stages
+// weight-ring stages of the layer3/4 halo tiles (A/B knobs): AVT_HALO_NST for the 128 x 128 tile (default 2:
+// two blocks per CU; 3 = one block: B=128 layer3/4 -12..-20 %), AVT_HALO_SMALL_NST for the 64 x 128
+// small-batch tile (default 3, still two blocks per CU: B=32 layer3 +3..16 %, vision layer4 +3..20 %;
+// 4 and 5 leave one block per CU and lose; tools/conv_bench.py --stages)
+static int g_halo_nst = -1, g_halo_small_nst = -1;  // -1: from the environment; avt_set_halo_stages
 static int halo_nst() {
   if (g_halo_nst < 0) g_halo_nst = getenv("AVT_HALO_NST") ? atoi(getenv("AVT_HALO_NST")) : 2;
   return g_halo_nst;
 }
 static int halo_small_nst() {
-  if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 2;
+  if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 3;
   return g_halo_small_nst;
 }
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)

@@ -88,6 +88,11 @@ class ResNet(nn.Module):
             return False
         return name != ("conv1.weight" if self.modal == "audio" else "conv1_a.weight")
 
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_avt_engine"] = None
+        return state
+
     def _adopt(self, parent, prefix: str):
         """Called by the owning AVENet once its flat store holds this trunk's parameters."""
         self._avt_parent = (weakref.ref(parent), prefix)
@@ -278,6 +283,11 @@ class AVENet(nn.Module):
         self._engines = {}
         for prefix, net in (("imgnet.", self.imgnet), ("audnet.", self.audnet)):
             net._adopt(self, prefix)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_engines"] = {}  # device state (streams, packed weights) is rebuilt, never copied
+        return state
 
     def __setstate__(self, state):
         """copy.deepcopy / unpickling: the trunks must point at this copy's flat store, not the original's
@@ -503,6 +513,11 @@ class FullModel(nn.Module):
         self._flat = FlatStore(self, tube_trainable)
         self._engine = None
         self.audnet._adopt(self, "audnet.")
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_engine"] = None
+        return state
 
     def __setstate__(self, state):
         """copy.deepcopy / unpickling: re-adopt the audio trunk (see AVENet.__setstate__)."""

@@ -37,6 +37,16 @@ FULL_BUFS = [p + s for p in ("imgnet.", "audnet.") for s in
 TUBE_BUFS = ["audnet.bn1", "audnet.layer1.0.bn1", "audnet.layer4.1.bn2", "vidnet.bn1", "vidnet.layer4.1.bn2"]
 
 
+SAMPLE = 256  # strided gradient sample per parameter (direction checks of every parameter)
+
+
+def grad_sample(g: torch.Tensor) -> np.ndarray:
+    """SAMPLE values of a gradient at a fixed stride over the whole tensor (all of it when smaller)."""
+    f = g.detach().flatten()
+    stride = max(1, f.numel() // SAMPLE)
+    return f[::stride][:SAMPLE].double().numpy()
+
+
 def _peak_gb():
     return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2 ** 20
 
@@ -97,6 +107,8 @@ def avenet_fixture(ref_model, name, batch, seed_w=0):
     out["grad_norm_f64"] = g64
     for n in SLICE_PARAMS:
         out["grad_slice_f64/" + n] = grads[n].flatten()[:64].numpy()
+    for n in names:
+        out["grad_sample_f64/" + n] = grad_sample(grads[n])
     for b in FULL_BUFS:
         out["buf_f64/" + b + ".running_mean"] = bufs[b + ".running_mean"].numpy()
         out["buf_f64/" + b + ".running_var"] = bufs[b + ".running_var"].numpy()
@@ -120,6 +132,10 @@ def avenet_fixture(ref_model, name, batch, seed_w=0):
     }
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
+    for n in SLICE_PARAMS:  # the yardstick's own gradient values (direction bounds of the GPU test)
+        out["bf16ref_slice/" + n] = rb["grads"][n].flatten()[:64].double().numpy()
+    for n in names:
+        out["bf16ref_sample/" + n] = grad_sample(rb["grads"][n])
     for bn, (em, ev) in bn_stat_dev(rb["bufs"], bufs, FULL_BUFS).items():
         out["bf16ref_dev/bnstat/" + bn] = np.array([em, ev])
         print(f"[{name}] bf16-trunk reference {bn}: batch-mean err {em:.2e} of std, batch-var rel err {ev:.2e}")
@@ -177,6 +193,8 @@ def tube_fixture(ref_model, name, b, t, seed_w=0):
     out.update(A_f64=A.detach().numpy(), logits_f64=logits.detach().numpy(), loss_f64=loss.detach().numpy())
     g64 = np.array([grads[n].norm().item() for n in names])
     out["grad_norm_f64"] = g64
+    for n in names:
+        out["grad_sample_f64/" + n] = grad_sample(grads[n])
     for bn in TUBE_BUFS:
         out["buf_f64/" + bn + ".running_mean"] = bufs[bn + ".running_mean"].numpy()
         out["buf_f64/" + bn + ".running_var"] = bufs[bn + ".running_var"].numpy()
@@ -199,6 +217,8 @@ def tube_fixture(ref_model, name, b, t, seed_w=0):
     }
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
+    for n in names:
+        out["bf16ref_sample/" + n] = grad_sample(rb["grads"][n])
     for bn, (em, ev) in bn_stat_dev(rb["bufs"], bufs, TUBE_BUFS).items():
         out["bf16ref_dev/bnstat/" + bn] = np.array([em, ev])
         print(f"[{name}] bf16-trunk reference {bn}: batch-mean err {em:.2e} of std, batch-var rel err {ev:.2e}")

@@ -325,7 +325,11 @@ def test_dataparallel_replica_matches_model(mirror):
         eng = AVEngine(model._flat.mirror(DEV), model.epsilon, model.epsilon2, model.tau, model.trimap, model.Neg)
     l_dp, g_dp = _dp_grads(model, img, aud, eng)
     assert rel_err(l_dp, logits.detach()) < 1e-5
-    assert set(g_dp) == set(ref)
+    # replicate()'s Broadcast hands every parameter a gradient: zeros for the ones the step never uses
+    # (fc, conv1_flow, the other stems) -- as torch's DataParallel does on >1 GPU
+    assert set(ref) <= set(g_dp)
+    for n in set(g_dp) - set(ref):
+        assert not g_dp[n].any(), n
     for n in ref:  # same kernels, same inputs: only atomic-order noise
         assert rel_err(g_dp[n], ref[n]) < 2e-3, (n, rel_err(g_dp[n], ref[n]))
     if mirror:  # a replica on another GPU does not touch the module's BN running statistics

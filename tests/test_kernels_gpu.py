@@ -240,7 +240,7 @@ def test_halo_stages_bitwise_equal(case):
                 assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
                 torch.testing.assert_close(o[2], outs[0][2], rtol=1e-9, atol=1e-6)
     finally:
-        call("avt_set_halo_stages", 2, 2)
+        call("avt_set_halo_stages", 2, 3)
         call("avt_set_small_tiles", 1)
 
 

@@ -123,7 +123,7 @@ def main():
                 ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
                                          pad, S()))
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
-            call("avt_set_halo_stages", 2, 2)
+            call("avt_set_halo_stages", 2, 3)
         if (args.nt64 or args.nt128) and args.halo:
             call("avt_set_halo", 0)  # the tap-gather configs on every shape
         if args.nt64 and K == 64 or args.nt64 and C == 64:
