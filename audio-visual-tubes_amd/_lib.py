@@ -94,9 +94,10 @@ SIGNATURES = {
     "avt_hardway_attention_fwd": (_I, [_P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "avt_hardway_attention_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
     "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
-    "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
-    "avt_npratio_loss": (_I, [_P, _I, _I, _I, _P, _P, _P]),
-    "avt_flip_l1_loss": (_I, [_P, _P, _L, _I, _P, _P, _P, _P]),
+    "avt_loss_workspace_floats": (_Z, [_L, _L]),
+    "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
+    "avt_npratio_loss": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
+    "avt_flip_l1_loss": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _P]),
     "avt_localize_ciou": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "avt_pair_ciou": (_I, [_P, _I, _I, _P, _P]),
     "avt_spectrogram_segments": (_I, [_L, _I]),

@@ -1149,6 +1149,12 @@ struct WgradPlan {
 };
 
 static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
+  static bool env_read = false;  // A/B knobs: AVT_WGRAD_SLAB_MAX, AVT_WGRAD_WAVE_COST (as avt_set_wgrad_slab_max)
+  if (!env_read) {
+    env_read = true;
+    if (const char* e = getenv("AVT_WGRAD_SLAB_MAX")) g_wgrad_slab_max = atoi(e);
+    if (const char* e = getenv("AVT_WGRAD_WAVE_COST")) g_wgrad_wave_cost = atoi(e);
+  }
   WgradPlan pl{};
   GemmTNParams& p = pl.p;
   p.Mg = K;

@@ -539,13 +539,31 @@ __global__ __launch_bounds__(1024) void twoview_loss_kernel(const float* __restr
 }
 
 // ---- PropagationLoss (losses.py:16-23) on x [b][t][P]: loss and d(loss)/dx, one block ----
-__global__ __launch_bounds__(1024) void propagation_loss_kernel(const float* __restrict__ x, int b, int t, int P,
-                                                                float* __restrict__ loss, float* __restrict__ dx) {
+// ---- losses.py on a multi-block grid: every element's gradient in one grid-stride pass, each block's
+// partial |.| sum into ws[block], then ONE block sums ws[0..nblk) in a fixed order (deterministic) ----
+constexpr int kLossMaxBlocks = 1024;
+
+__device__ __forceinline__ void block_partial(float a, float* red, float* ws) {
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) ws[blockIdx.x] = a;
+}
+
+// loss = scale * sum_{i < n} ws[i], summed by one block in a fixed order
+__global__ __launch_bounds__(256) void loss_finish_kernel(const float* __restrict__ ws, int n, float scale,
+                                                          float* __restrict__ loss) {
   __shared__ float red[16];
-  const long long n = (long long)b * t * P;
-  const float k = 1.f / ((float)b * (float)(t - 1) * (float)P);
   float a = 0.f;
-  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) a += ws[i];
+  a = block_sum(a, red);
+  if (threadIdx.x == 0) *loss = a * scale;
+}
+
+// PropagationLoss (losses.py:16-23) on x [b][t][P]: mean over (b, s < t-1, p) of |x[b,s+1,p] - x[b,s,p]|
+__global__ __launch_bounds__(256) void propagation_loss_kernel(const float* __restrict__ x, int t, int P, long long n,
+                                                               float k, float* __restrict__ dx, float* __restrict__ ws) {
+  __shared__ float red[16];
+  float a = 0.f;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const int s = (int)((e / P) % t);
     float g = 0.f;
     if (s + 1 < t) {
@@ -556,34 +574,34 @@ __global__ __launch_bounds__(1024) void propagation_loss_kernel(const float* __r
     if (s > 0) g += sgnf(x[e] - x[e - P]) * k;
     if (dx) dx[e] = g;
   }
-  a = block_sum(a, red);
-  if (threadIdx.x == 0) *loss = a * k;
+  block_partial(a, red, ws);
 }
 
 // ---- NPRatio (losses.py:7-14) on x [b][t][P]: loss = mean_b mean_s |S[b,s+1] - S[b,s]|, S = sum_p x ----
-// one block; S kept in LDS (b*t <= kNpMaxRows); dx[b,s,p] = dloss/dS[b,s] for every p
-constexpr int kNpMaxRows = 4096;
-__global__ __launch_bounds__(1024) void npratio_loss_kernel(const float* __restrict__ x, int b, int t, int P,
-                                                            float* __restrict__ loss, float* __restrict__ dx) {
-  __shared__ float S[kNpMaxRows];
-  __shared__ float red[16];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int rows = b * t;
-  for (int r = w; r < rows; r += nw) {
+// pass 1: S[r] (one wave per row) into ws; pass 2: dx[b,s,p] = dloss/dS[b,s] for every p, and the
+// per-block partial sums of |S[r+1] - S[r]| over the rows the block's first elements start
+__global__ __launch_bounds__(256) void npratio_rows_kernel(const float* __restrict__ x, int rows, int P,
+                                                           float* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < rows; r += nw) {
     float a = 0.f;
     for (int p = lane; p < P; p += 64) a += x[(size_t)r * P + p];
     a = wave_sum(a);
     if (lane == 0) S[r] = a;
   }
-  __syncthreads();
-  const float k = 1.f / ((float)b * (float)(t - 1));
+}
+
+__global__ __launch_bounds__(256) void npratio_loss_kernel(const float* __restrict__ S, int rows, int t, int P,
+                                                           float k, float* __restrict__ dx, float* __restrict__ ws) {
+  __shared__ float red[16];
   float acc = 0.f;
-  for (int r = threadIdx.x; r < rows; r += blockDim.x)
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x)
     if (r % t + 1 < t) acc += fabsf(S[r + 1] - S[r]);
-  acc = block_sum(acc, red);
-  if (threadIdx.x == 0) *loss = acc * k;
+  block_partial(acc, red, ws);
   if (dx) {
-    for (long long e = threadIdx.x; e < (long long)rows * P; e += blockDim.x) {
+    const long long n = (long long)rows * P;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
       const int r = (int)(e / P), s = r % t;
       float g = 0.f;
       if (s + 1 < t) g -= sgnf(S[r + 1] - S[r]) * k;
@@ -595,14 +613,12 @@ __global__ __launch_bounds__(1024) void npratio_loss_kernel(const float* __restr
 
 // ---- FlipLoss (losses.py:25-36): nn.L1Loss()(y, hflip(x)) over rows of W (the last dim) ----
 // loss = mean |y[r,w] - x[r,W-1-w]|; dy = sgn(.)/n, dx[r,W-1-w] = -sgn(.)/n (sgn(0) = 0, as torch)
-__global__ __launch_bounds__(1024) void flip_l1_loss_kernel(const float* __restrict__ x, const float* __restrict__ y,
-                                                            long long rows, int W, float* __restrict__ loss,
-                                                            float* __restrict__ dx, float* __restrict__ dy) {
+__global__ __launch_bounds__(256) void flip_l1_loss_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                           long long n, int W, float inv_n, float* __restrict__ dx,
+                                                           float* __restrict__ dy, float* __restrict__ ws) {
   __shared__ float red[16];
-  const long long n = rows * W;
-  const float inv_n = 1.f / (float)n;
   float acc = 0.f;
-  for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const long long r = e / W;
     const int wc = (int)(e - r * W);
     const long long ef = r * W + (W - 1 - wc);
@@ -611,8 +627,12 @@ __global__ __launch_bounds__(1024) void flip_l1_loss_kernel(const float* __restr
     if (dy) dy[e] = sgnf(d) * inv_n;
     if (dx) dx[ef] = -sgnf(d) * inv_n;
   }
-  acc = block_sum(acc, red);
-  if (threadIdx.x == 0) *loss = acc * inv_n;
+  block_partial(acc, red, ws);
+}
+
+static int loss_blocks(long long n) {
+  long long b = (n + 1023) / 1024;  // ~4 elements per thread
+  return (int)(b < 1 ? 1 : (b > kLossMaxBlocks ? kLossMaxBlocks : b));
 }
 
 __global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int n) {
@@ -775,28 +795,53 @@ extern "C" int avt_twoview_loss(const float* ce1, const float* ce2, const float*
   return check_launch("twoview_loss");
 }
 
-// PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (optional) = d(loss)/dx.
-extern "C" int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream) {
-  AVT_REQUIRE(x && loss, "propagation_loss: null pointer");
+// scratch floats the three losses below need: per-block partial sums (+ NPRatio's row sums S)
+extern "C" size_t avt_loss_workspace_floats(long long n, long long rows) {
+  return (size_t)kLossMaxBlocks + (size_t)(rows > 0 ? rows : 0);
+}
+
+// PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (optional) = d(loss)/dx.  ws: avt_loss_workspace_floats.
+extern "C" int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, float* ws,
+                                    void* stream) {
+  AVT_REQUIRE(x && loss && ws, "propagation_loss: null pointer");
   AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "propagation_loss: need b >= 1, t >= 2, P >= 1 (b=%d t=%d P=%d)", b, t, P);
-  hipLaunchKernelGGL(propagation_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, b, t, P, loss, dx);
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = (long long)b * t * P;
+  const float k = 1.f / ((float)b * (float)(t - 1) * (float)P);
+  const int nb = loss_blocks(n);
+  hipLaunchKernelGGL(propagation_loss_kernel, dim3(nb), dim3(256), 0, st, x, t, P, n, k, dx, ws);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(256), 0, st, ws, nb, k, loss);
   return check_launch("propagation_loss");
 }
 
-// NPRatio (losses.py:7-14) of x [b][t][P]; dx (optional) = d(loss)/dx.
-extern "C" int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream) {
-  AVT_REQUIRE(x && loss, "npratio_loss: null pointer");
+// NPRatio (losses.py:7-14) of x [b][t][P]; dx (optional) = d(loss)/dx.  ws: avt_loss_workspace_floats(n, b*t).
+extern "C" int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, float* ws,
+                                void* stream) {
+  AVT_REQUIRE(x && loss && ws, "npratio_loss: null pointer");
   AVT_REQUIRE(b >= 1 && t >= 2 && P >= 1, "npratio_loss: need b >= 1, t >= 2, P >= 1 (b=%d t=%d P=%d)", b, t, P);
-  AVT_REQUIRE((long long)b * t <= kNpMaxRows, "npratio_loss: b*t=%d exceeds %d", b * t, kNpMaxRows);
-  hipLaunchKernelGGL(npratio_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, b, t, P, loss, dx);
+  hipStream_t st = (hipStream_t)stream;
+  const int rows = b * t;
+  const float k = 1.f / ((float)b * (float)(t - 1));
+  float* S = ws + kLossMaxBlocks;
+  const int rb = (int)((rows + 3) / 4 < 4096 ? (rows + 3) / 4 : 4096);  // 4 waves per block, one row each
+  hipLaunchKernelGGL(npratio_rows_kernel, dim3(rb), dim3(256), 0, st, x, rows, P, S);
+  const int nb = loss_blocks((long long)rows * P);
+  hipLaunchKernelGGL(npratio_loss_kernel, dim3(nb), dim3(256), 0, st, S, rows, t, P, k, dx, ws);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(256), 0, st, ws, nb, k, loss);
   return check_launch("npratio_loss");
 }
 
-// FlipLoss (losses.py:25-36): L1(y, hflip(x)) over `rows` rows of W; dx / dy (optional) gradients.
+// FlipLoss (losses.py:25-36): nn.L1Loss()(y, hflip(x)) over `rows` rows of W; dx / dy (optional) gradients.
 extern "C" int avt_flip_l1_loss(const float* x, const float* y, long long rows, int W, float* loss, float* dx,
-                                float* dy, void* stream) {
-  AVT_REQUIRE(x && y && loss, "flip_l1_loss: null pointer");
+                                float* dy, float* ws, void* stream) {
+  AVT_REQUIRE(x && y && loss && ws, "flip_l1_loss: null pointer");
   AVT_REQUIRE(rows >= 1 && W >= 1, "flip_l1_loss: empty input");
-  hipLaunchKernelGGL(flip_l1_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, y, rows, W, loss, dx, dy);
+  hipStream_t st = (hipStream_t)stream;
+  const long long n = rows * W;
+  const float inv_n = 1.f / (float)n;
+  const int nb = loss_blocks(n);
+  hipLaunchKernelGGL(flip_l1_loss_kernel, dim3(nb), dim3(256), 0, st, x, y, n, W, inv_n, dx, dy, ws);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(256), 0, st, ws, nb, inv_n, loss);
   return check_launch("flip_l1_loss");
 }
+

@@ -7,14 +7,22 @@ forward launch and scaled by the upstream gradient in backward.
   mean over (clip, frame pair) of |sum_hw heatmap[:, s+1] - sum_hw heatmap[:, s]|.
 * ``FlipLoss()(heatmap, flipped_heatmap)`` (losses.py:25-36): nn.L1Loss()(flipped_heatmap,
   RandomHorizontalFlip(p=1)(heatmap)), the flip along the last dimension.
+
+Each runs on a multi-block grid (no size limit): gradients elementwise, the loss as per-block partial
+sums that one block adds in a fixed order (deterministic, run to run).
 """
 from __future__ import annotations
 
 import torch
 from torch import nn
 
-from ._lib import call
+from ._lib import call, query
 from .trunk import P, stream_ptr
+
+
+def _workspace(x: torch.Tensor, rows: int = 0) -> torch.Tensor:
+    """Scratch of the multi-block loss kernels (per-block partial sums, NPRatio's row sums)."""
+    return torch.empty(int(query("avt_loss_workspace_floats", x.numel(), rows)), device=x.device, dtype=torch.float32)
 
 
 class _PropagationLossFn(torch.autograd.Function):
@@ -30,7 +38,7 @@ class _PropagationLossFn(torch.autograd.Function):
         x = heatmap.detach().contiguous().float()
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         dx = torch.empty_like(x) if heatmap.requires_grad else None
-        call("avt_propagation_loss", P(x), b, t, h * w, P(loss), P(dx), stream_ptr())
+        call("avt_propagation_loss", P(x), b, t, h * w, P(loss), P(dx), P(_workspace(x)), stream_ptr())
         ctx.save_for_backward(dx)
         ctx.in_dtype = heatmap.dtype
         return loss.to(heatmap.dtype)
@@ -61,7 +69,7 @@ class _NPRatioFn(torch.autograd.Function):
         x = heatmap.detach().contiguous().float()
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         dx = torch.empty_like(x) if heatmap.requires_grad else None
-        call("avt_npratio_loss", P(x), b, t, h * w, P(loss), P(dx), stream_ptr())
+        call("avt_npratio_loss", P(x), b, t, h * w, P(loss), P(dx), P(_workspace(x, b * t)), stream_ptr())
         ctx.save_for_backward(dx)
         ctx.in_dtype = heatmap.dtype
         return loss.to(heatmap.dtype)
@@ -93,7 +101,7 @@ class _FlipLossFn(torch.autograd.Function):
         loss = torch.empty((), device=x.device, dtype=torch.float32)
         dx = torch.empty_like(x) if heatmap.requires_grad else None
         dy = torch.empty_like(y) if flipped.requires_grad else None
-        call("avt_flip_l1_loss", P(x), P(y), x.numel() // W, W, P(loss), P(dx), P(dy), stream_ptr())
+        call("avt_flip_l1_loss", P(x), P(y), x.numel() // W, W, P(loss), P(dx), P(dy), P(_workspace(x)), stream_ptr())
         ctx.save_for_backward(dx, dy)
         ctx.dtypes = (heatmap.dtype, flipped.dtype)
         return loss.to(flipped.dtype)

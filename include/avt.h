@@ -276,13 +276,16 @@ int avt_hardway_attention_bwd(const float* v, const float* an, const float* inv,
  * dwA1/dwA2 = d(combined)/d(weighted_A).  losses.py:16-23 PropagationLoss + nn.MSELoss. */
 int avt_twoview_loss(const float* ce1, const float* ce2, const float* wA1, const float* wA2, int b, int t, int P,
                      float loss_weight, float* out, float* dwA1, float* dwA2, void* stream);
+/* Scratch (floats) of the three losses below for n elements / `rows` rows (NPRatio: b*t): per-block
+ * partial sums, summed by one block in a fixed order (deterministic) -- and NPRatio's row sums */
+size_t avt_loss_workspace_floats(long long n, long long rows);
 /* PropagationLoss (losses.py:16-23) of x [b][t][P]; dx (or NULL) = d(loss)/dx */
-int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
-/* NPRatio (losses.py:7-14) of x [b][t][P] (b*t <= 4096): mean |diff_t sum_p x|; dx (or NULL) = d(loss)/dx */
-int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, void* stream);
+int avt_propagation_loss(const float* x, int b, int t, int P, float* loss, float* dx, float* ws, void* stream);
+/* NPRatio (losses.py:7-14) of x [b][t][P]: mean |diff_t sum_p x|; dx (or NULL) = d(loss)/dx */
+int avt_npratio_loss(const float* x, int b, int t, int P, float* loss, float* dx, float* ws, void* stream);
 /* FlipLoss (losses.py:25-36): nn.L1Loss()(y, hflip(x)) over `rows` rows of W; dx, dy (or NULL) gradients */
 int avt_flip_l1_loss(const float* x, const float* y, long long rows, int W, float* loss, float* dx, float* dy,
-                     void* stream);
+                     float* ws, void* stream);
 
 /* ---- localisation metrics (test loops of train_hardway*.py / test.py; utils.py:203-239, 311-318) ---- */
 /* A [N][h][w] heatmaps -> cv2 INTER_LINEAR resize to S x S, normalize_img(-.), 1 - ., median

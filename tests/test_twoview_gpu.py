@@ -150,7 +150,7 @@ def test_propagation_loss_module():
     assert rel_err(xd.grad, xr.grad) < 1e-6
 
 
-@pytest.mark.parametrize("b,t", [(3, 5), (8, 16), (1, 2)])
+@pytest.mark.parametrize("b,t", [(3, 5), (8, 16), (1, 2), (300, 16)])
 def test_npratio_loss_module(b, t):
     """losses.NPRatio (losses.py:7-14; train_3D.py:113, 135) vs its torch restatement in fp64."""
     from avt_amd.losses import NPRatio
@@ -169,7 +169,7 @@ def test_npratio_loss_module(b, t):
     assert rel_err(xd.grad, xr.grad) < 1e-6
 
 
-@pytest.mark.parametrize("shape", [(4, 1, 14, 14), (2, 3, 7, 9), (5, 224)])
+@pytest.mark.parametrize("shape", [(4, 1, 14, 14), (2, 3, 7, 9), (5, 224), (64, 1, 224, 224)])
 def test_flip_loss_module(shape):
     """losses.FlipLoss (losses.py:25-36): L1(flipped, hflip(heatmap)) and both gradients, fp64 ref."""
     from avt_amd.losses import FlipLoss
@@ -185,6 +185,8 @@ def test_flip_loss_module(shape):
     (0.7 * ref).backward()
     assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
     assert rel_err(xd.grad, xr.grad) < 1e-6 and rel_err(yd.grad, yr.grad) < 1e-6
+    # a multi-block grid (a full-resolution batch is 3.2 M elements) with a fixed-order reduction
+    assert FlipLoss()(xd, yd).item() == loss.item()
 
 
 # ------------------------------------------------------------------------------ whole step
