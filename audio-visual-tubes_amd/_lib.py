@@ -63,6 +63,10 @@ SIGNATURES = {
     "avt_conv2d_dgrad_bn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(DgradBnEpi), _P]),
     "avt_bn_bwd_premasked": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "avt_conv2d_dgrad_mask": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_conv2d_splitk_plan": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "avt_set_halo_splitk": (_I, [_I, _I]),
+    "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "avt_bn_bwd_mask": (_I, [_P, _P, ctypes.POINTER(BnBwdTarget), ctypes.POINTER(BnBwdTarget), _L, _I, _P]),
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
@@ -105,6 +109,8 @@ SIGNATURES = {
     "avt_frames_transform": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P]),
     "avt_adam_step": (_I, [_P, _P, _P, _P, _L, _F, _F, _F, _F, _F, _F, _I, _P]),
     "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _P, _P, _P, _P]),
+    "avt_adam_prep_dev": (_I, [_P, _P, _P, _P]),
+    "avt_adam_apply_dev": (_I, [_P, _P, _P, _P, _L, _F, _P, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_pack_desc_bytes": (_Z, []),
     "avt_pack_conv_weights_batched": (_I, [_P, _I, _L, _P]),

@@ -602,7 +602,7 @@ extern "C" int avt_set_halo(int on) {
 }
 
 extern "C" int avt_set_halo_stages(int nst128, int nst64) {
-  AVT_REQUIRE(nst128 >= 2 && nst128 <= 3 && nst64 >= 2 && nst64 <= 5, "set_halo_stages: nst128 in 2..3, nst64 in 2..5");
+  AVT_REQUIRE(nst128 >= 2 && nst128 <= 5 && nst64 >= 2 && nst64 <= 5, "set_halo_stages: nst128, nst64 in 2..5");
   avt::g_halo_nst = nst128;
   avt::g_halo_small_nst = nst64;
   return AVT_OK;
@@ -813,9 +813,14 @@ static bool use_small_tile(const GemmNTParams& p, int BN) {
 }
 
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR>
-static void launch_halo(const GemmNTParams& p, hipStream_t st) {
+static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, float* part = nullptr,
+                        int* cnt = nullptr) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   HaloArgs ha{};
+  ha.ksplit = ksplit;
+  ha.cps = p.IC / 64 / ksplit;
+  ha.part = part;
+  ha.cnt = cnt;
   const int batch = p.M / (p.OH * p.OW);
   ha.act_bytes = (unsigned)((size_t)batch * p.IH * p.IW * p.IC * 2);
   ha.w_bytes = (unsigned)((size_t)p.Ng * p.Kg * 2);
@@ -830,13 +835,71 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st) {
       ha.tap_disp[t] = dy * p.OW + dx;
       ha.tap_w[t] = t;
     }
-  const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
+  const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN) * ksplit;
+  if (grid > 0 && ksplit > 1) {
+    hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, true>), dim3(grid),
+                       dim3(WM * WN * 64), 0, st, p, ha);
+    return;
+  }
   if (grid > 0 && MODE == MODE_DGRAD && p.bx != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>), dim3(grid), dim3(WM * WN * 64), 0,
                        st, p, ha);
   else if (grid > 0)
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX>), dim3(grid), dim3(WM * WN * 64), 0, st,
                        p, ha);
+}
+
+// the 4-wave 128 x 128 halo tile by weight-ring depth (avt_set_halo_stages / AVT_HALO_NST): 2 stages (80 KB
+// LDS, 2 blocks per CU; one 16 KiB weight stage in flight behind each step's 16 MFMAs per wave) or 3-5
+// (96-128 KB, 1 block per CU; NSTB-1 stages in flight)
+template <int MODE>
+static void launch_halo128(const GemmNTParams& p, hipStream_t st, int ks = 1, float* part = nullptr,
+                           int* cnt = nullptr) {
+  switch (halo_nst()) {
+    case 3: launch_halo<MODE, 2, 2, 2, 2, 3, 168>(p, st, ks, part, cnt); break;
+    case 4: launch_halo<MODE, 2, 2, 2, 2, 4, 168>(p, st, ks, part, cnt); break;
+    case 5: launch_halo<MODE, 2, 2, 2, 2, 5, 168>(p, st, ks, part, cnt); break;
+    default: launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st, ks, part, cnt); break;
+  }
+}
+
+// ---- split-K for the 128 x 128 halo tile (layer3/4 at a few clips per GPU) ----
+// A 128-row grid of fewer blocks than the chip holds leaves CUs idle, and the 64-row tile that fills
+// it moves twice the weight bytes per FLOP through L2 -> LDS.  Split-K keeps the 128 x 128 tile and
+// gives each of `ksplit` blocks per tile a range of the 64-channel chunks; the last block to finish a
+// tile sums the fp32 partials (conv_halo.h).  Plan: ksplit = the smallest divisor of the chunk count
+// whose grid reaches g_splitk_blocks (AVT_SPLITK_BLOCKS, default 2 blocks per CU); AVT_HALO_SPLITK /
+// avt_set_halo_splitk(s > 0) forces the largest divisor <= s, 1 turns it off.
+static int g_halo_splitk = -1, g_splitk_blocks = -1;
+struct SplitWs {
+  float* part;
+  int* cnt;
+};
+static bool halo_splitk_shape(const GemmNTParams& p) {
+  return halo_eligible(p) && conv_variant() == 1 && p.Ng % 128 == 0 && 128 + 2 * p.OW + 2 <= 168 &&
+         p.bx == nullptr;
+}
+static int halo_splitk(const GemmNTParams& p) {
+  if (g_halo_splitk < 0) g_halo_splitk = getenv("AVT_HALO_SPLITK") ? atoi(getenv("AVT_HALO_SPLITK")) : 0;
+  if (g_splitk_blocks < 0)
+    g_splitk_blocks = getenv("AVT_SPLITK_BLOCKS") ? atoi(getenv("AVT_SPLITK_BLOCKS")) : 2 * num_cus();
+  if (!halo_splitk_shape(p)) return 1;
+  const int nchunk = p.IC / 64;
+  const long long tiles = (long long)((p.M + 127) / 128) * (p.Ng / 128);
+  if (g_halo_splitk > 0) {
+    int s = 1;
+    for (int d = 1; d <= nchunk && d <= g_halo_splitk; ++d)
+      if (nchunk % d == 0) s = d;
+    return s;
+  }
+  if (tiles >= g_splitk_blocks) return 1;
+  int s = 1;
+  for (int d = 2; d <= nchunk; ++d)
+    if (nchunk % d == 0) {
+      s = d;
+      if (tiles * d >= g_splitk_blocks) break;
+    }
+  return s;
 }
 
 // C = K = 64 3x3/s1/p1 Conv2d (the layer-1 convs), image width <= 95, not a BN-epilogue dgrad and not
@@ -897,10 +960,17 @@ static void launch_c64(const GemmNTParams& p, hipStream_t st) {
 }
 
 template <int MODE, int CVEC, int BM, int BN>
-static void launch_nt(const GemmNTParams& p, hipStream_t st) {
+static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws = nullptr) {
   if (CVEC == 8 && c64_eligible(p)) {
     launch_c64<MODE>(p, st);
     return;
+  }
+  if (CVEC == 8 && ws != nullptr && p.IT == 1 && p.OT == 1) {
+    const int ks = halo_splitk(p);
+    if (ks > 1) {
+      launch_halo128<MODE>(p, st, ks, ws->part, ws->cnt);
+      return;
+    }
   }
   if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && g_nt64_config == 1 &&
       p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
@@ -932,10 +1002,8 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
     }
     else if (g_halo == 2)
       launch_halo<MODE, 4, 2, 2, 1>(p, st);  // 256 x 64, 8 waves (A/B only)
-    else if (halo_nst() == 3)
-      launch_halo<MODE, 2, 2, 2, 2, 3, 168>(p, st);  // 128 x 128, 3 weight stages: 96 KB LDS, 1 block per CU
     else
-      launch_halo<MODE, 2, 2, 2, 2, 2, 168>(p, st);  // 128 x 128, 4 waves, 80 KB LDS: 2 blocks per CU
+      launch_halo128<MODE>(p, st);  // 128 x 128, 4 waves
     return;
   }
   if (CVEC == 8 && conv_variant() == 1) {
@@ -973,8 +1041,58 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st) {
 
 extern "C" int avt_bn_slots(void) { return AVT_BN_SLOTS; }
 
+static int conv2d_fwd_impl(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp,
+                           int K, int R, int S, int stride, int pad, int Kg, const SplitWs* ws, void* stream);
+
 extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W,
                               int Cp, int K, int R, int S, int stride, int pad, int Kg, void* stream) {
+  return conv2d_fwd_impl(x, wpack, y, bn_acc, N, H, W, Cp, K, R, S, stride, pad, Kg, nullptr, stream);
+}
+
+// split-K workspace of a 3x3/s1 conv (halo kernel): *part_floats fp32 partials, *counters ints (zero
+// before the first launch; the kernel leaves them zero).  Both 0: the shape runs without split-K.
+extern "C" int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int dgrad,
+                                      long long* part_floats, int* counters) {
+  AVT_REQUIRE(part_floats && counters, "conv2d_splitk_plan: null pointer");
+  *part_floats = 0;
+  *counters = 0;
+  GemmNTParams p{};
+  p.IT = p.OT = p.KT = 1;
+  p.R = R; p.S = S; p.stride = stride; p.pad = pad;
+  if (dgrad) {
+    p.IH = conv_out(H, R, stride, pad); p.IW = conv_out(W, S, stride, pad); p.IC = K;
+    p.OH = H; p.OW = W; p.Ng = C;
+  } else {
+    p.IH = H; p.IW = W; p.IC = C;
+    p.OH = conv_out(H, R, stride, pad); p.OW = conv_out(W, S, stride, pad); p.Ng = K;
+  }
+  p.M = N * p.OH * p.OW;
+  if (p.IC % 64 != 0 || p.Ng % 64 != 0 || p.M <= 0) return AVT_OK;
+  const int ks = halo_splitk(p);
+  if (ks <= 1) return AVT_OK;
+  const int tiles = ((p.M + 127) / 128) * (p.Ng / 128);
+  *part_floats = (long long)tiles * ks * 128 * 128;
+  *counters = tiles;
+  return AVT_OK;
+}
+
+extern "C" int avt_set_halo_splitk(int ksplit, int target_blocks) {
+  AVT_REQUIRE(ksplit >= 0 && target_blocks >= 0, "set_halo_splitk: bad arguments");
+  g_halo_splitk = ksplit;
+  g_splitk_blocks = target_blocks > 0 ? target_blocks : 2 * num_cus();
+  return AVT_OK;
+}
+
+extern "C" int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W,
+                                 int Cp, int K, int R, int S, int stride, int pad, int Kg, float* part, int* cnt,
+                                 void* stream) {
+  const SplitWs ws{part, cnt};
+  return conv2d_fwd_impl(x, wpack, y, bn_acc, N, H, W, Cp, K, R, S, stride, pad, Kg, (part && cnt) ? &ws : nullptr,
+                         stream);
+}
+
+static int conv2d_fwd_impl(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp,
+                           int K, int R, int S, int stride, int pad, int Kg, const SplitWs* ws, void* stream) {
   AVT_REQUIRE(x && wpack && y, "conv2d_fwd: null pointer");
   AVT_REQUIRE(K % 64 == 0, "conv2d_fwd: K=%d must be a multiple of 64", K);
   AVT_REQUIRE(Kg % 32 == 0 && Kg >= R * S * Cp, "conv2d_fwd: Kg=%d must be a multiple of 32 >= R*S*C", Kg);
@@ -1028,7 +1146,7 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
   } else if (Cp == 1) {
     launch_nt<MODE_FWD, 1, 128, 64>(p, st);
   } else if (bn128) {
-    launch_nt<MODE_FWD, 8, 128, 128>(p, st);
+    launch_nt<MODE_FWD, 8, 128, 128>(p, st, ws);
   } else {
     launch_nt<MODE_FWD, 8, 128, 64>(p, st);
   }
@@ -1037,7 +1155,7 @@ extern "C" int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double*
 
 static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
                              int H, int W, int C, int K, int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi,
-                             void* stream) {
+                             void* stream, const SplitWs* ws = nullptr) {
   AVT_REQUIRE(dy && wt && dx, "conv2d_dgrad: null pointer");
   AVT_REQUIRE(epi == nullptr || (epi->xc && epi->stats && epi->acc), "conv2d_dgrad: epilogue needs xc, stats, acc");
   AVT_REQUIRE(epi == nullptr || epi->xc2 == nullptr || (epi->stats2 && epi->acc2),
@@ -1077,10 +1195,20 @@ static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const voi
   }
   hipStream_t st = (hipStream_t)stream;
   if (C % 128 == 0)
-    launch_nt<MODE_DGRAD, 8, 128, 128>(p, st);
+    launch_nt<MODE_DGRAD, 8, 128, 128>(p, st, ws);
   else
     launch_nt<MODE_DGRAD, 8, 128, 64>(p, st);
   return check_launch("conv2d_dgrad");
+}
+
+// avt_conv2d_dgrad / avt_conv2d_dgrad_mask (add_mask optional) with a split-K workspace
+extern "C" int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask,
+                                   int N, int H, int W, int C, int K, int R, int S, int stride, int pad, float* part,
+                                   int* cnt, void* stream) {
+  AVT_REQUIRE(add_mask == nullptr || (add && add != dx), "conv2d_dgrad_ws: add_mask needs add, not aliasing dx");
+  const SplitWs ws{part, cnt};
+  return conv2d_dgrad_impl(dy, wt, dx, add, add_mask, N, H, W, C, K, R, S, stride, pad, nullptr, stream,
+                           (part && cnt) ? &ws : nullptr);
 }
 
 extern "C" int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W,

@@ -22,7 +22,24 @@ struct HaloArgs {
   int tap_disp[9];       // input-pixel displacement dy*W + dx of each tap
   int tap_dy[9], tap_dx[9];
   int tap_w[9];          // weight tap index of each listed tap
+  // split-K (short grids: a few clips per GPU): ksplit blocks per output tile, each over cps of the
+  // 64-channel chunks; each stores its fp32 partial tile to part (register order, write-through) and
+  // takes a ticket on cnt[tile]; the last to arrive sums the ksplit partials in split order (so the
+  // result does not depend on arrival order), resets the ticket and runs the epilogue
+  int ksplit, cps;
+  float* part;           // [tiles][ksplit][BM*BN]
+  int* cnt;              // [tiles], zero between launches
 };
+
+// write-through (sc1) 16-byte stores / loads of the split-K partial tiles: the hand-off of
+// MI355X_MICROARCH.md's table (sc1 stores, every storing wave's vmcnt(0), a barrier, one agent-scope
+// atomic add per workgroup; the last adder reads with sc1 loads) -- no L2 write-back fence needed
+__device__ __forceinline__ void store_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 16);
+}
+__device__ __forceinline__ f32x4 load_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
 
 // WM x WN waves, each TM x TN 32x32 accumulators: BM = WM*TM*32 rows, BN = WN*TN*32 columns.
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
@@ -33,7 +50,7 @@ constexpr int halo_blocks_per_cu() {
   return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false>
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   constexpr int NW = WM * WN, NT = NW * 64;
@@ -62,12 +79,16 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   const int wm = wid / WN, wn = wid % WN;
   const int nnt = p.Ng / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = bid / nnt, nt = bid - mt * nnt;
+  // split-K: the split is the slowest index, so an XCD's blocks share one K range of the weights
+  const int ntile = SPLIT ? gridDim.x / ha.ksplit : gridDim.x;
+  const int split = SPLIT ? bid / ntile : 0, tile = bid - split * ntile;
+  const int mt = tile / nnt, nt = tile - mt * nnt;
   const int m0 = mt * BM, n0 = nt * BN;
   const int W = ha.W, H = ha.H, hw = W * H;
   const int pre = W + 1;  // patch row of output pixel m0 is pre
   const int PR = BM + 2 * pre;
-  const int nchunk = p.IC / BK;
+  const int nchunk = SPLIT ? ha.cps : p.IC / BK;  // chunks of this block's K range
+  const int cbase = SPLIT ? split * ha.cps : 0;
   const int S = nchunk * 9;
 
   if (tid < 128) reinterpret_cast<u32x4*>(zrow + (tid >> 6) * ABUF)[tid & 63] = u32x4{0u, 0u, 0u, 0u};
@@ -140,7 +161,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   auto issue = [&](int cn, int tn, int stage) {
     char* Bs = smem + 2 * ABUF + stage * BSTAGE;
     const bool live = cn < nchunk;
-    const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + cn * BK) * 2);
+    const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + (cbase + cn) * BK) * 2);
 #pragma unroll
     for (int i = 0; i < BR; ++i) buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
     if (tn >= NSTB - 1) {
@@ -151,7 +172,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const int q = ((tn - (NSTB - 1)) * AP + a) * NW + wid;  // pieces 0..6 of the patch
         const bool inrange = q < PINSTR;
         // out-of-range instructions still issue (constant vmcnt): zeros into the zero area
-        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, cn + 1) : kOOB);
+        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, cbase + cn + 1) : kOOB);
       }
     }
   };
@@ -165,7 +186,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
   // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2
-  for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, 0));
+  for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, cbase));
 #pragma unroll
   for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
@@ -230,6 +251,54 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   }
   wait_vmcnt<0>();
   __syncthreads();
+
+  if constexpr (SPLIT) {
+    // partial tile in register order: (wave, i, j, quarter) x 64 lanes x 16 B -- 1 KiB per instruction
+    const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(ha.part + (size_t)tile * ha.ksplit * BM * BN), (short)0, (int)(ha.ksplit * BM * BN * 4), 0x00020000);
+    auto poff = [&](int s, int i, int j, int q) -> unsigned {
+      return (unsigned)((((s * NW + wid) * TM + i) * TN + j) * 4 + q) * 1024u + lane * 16u;
+    };
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          store_wt16(rsp, poff(split, i, j, q),
+                     f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]});
+    wait_vmcnt<0>();  // this wave's partial has left for memory
+    __syncthreads();  // ... and every other wave's
+    int* flag = reinterpret_cast<int*>(red);
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(ha.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int ticket = flag[0];
+    __syncthreads();  // every wave has read it before the epilogue reuses the scratch
+    if (ticket != ha.ksplit - 1) return;  // not the last split of this tile
+    if (tid == 0) ha.cnt[tile] = 0;        // ready for the next launch
+    // sum the partials in split order (own one from registers): arrival order does not change the bits
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x16 tot;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) tot[v] = 0.f;
+        for (int s = 0; s < ha.ksplit; ++s) {
+          if (s == split) {
+            tot += acc[i][j];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x4 v4 = load_wt16(rsp, poff(s, i, j, q));
+#pragma unroll
+              for (int e = 0; e < 4; ++e) tot[4 * q + e] += v4[e];
+            }
+          }
+        }
+        acc[i][j] = tot;
+      }
+  }
 
   // ---- epilogue (as conv_nt_pipe_kernel): BN partial statistics, bf16 tile through LDS, (+ add) ----
   const int rows_valid = min(BM, p.M - m0);

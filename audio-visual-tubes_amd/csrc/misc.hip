@@ -307,6 +307,26 @@ extern "C" int avt_adam_step_dev(float* param, const float* grad, float* exp_avg
   return check_launch("adam_step_dev");
 }
 
+// avt_adam_step_dev in two parts, so that the update of a finished gradient region can run while the
+// backward still computes the rest (train.py, world 1): prep advances the device step counter and
+// writes coef once per step; apply updates one 16-byte-aligned region [param, param + n) from coef.
+extern "C" int avt_adam_prep_dev(const float* hyper, int* step, float* coef, void* stream) {
+  AVT_REQUIRE(hyper && step && coef, "adam_prep_dev: null pointer");
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, hyper, coef);
+  return check_launch("adam_prep_dev");
+}
+
+extern "C" int avt_adam_apply_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                                  float grad_scale, const float* coef, void* stream) {
+  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq && coef, "adam_apply_dev: null pointer");
+  AVT_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+              "adam_apply_dev: buffers must be 16-byte aligned");
+  if (n == 0) return AVT_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, n, grad_scale, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, coef);
+  return check_launch("adam_apply_dev");
+}
+
 extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd,
                                     void* out_dgrad, void* stream) {
   AVT_REQUIRE(w, "pack_conv_weight: null pointer");

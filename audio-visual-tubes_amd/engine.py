@@ -196,6 +196,9 @@ class _EngineStore(Store):
     def stat_acc(self, bn, kind):
         return self.e.stat_views[(bn.prefix, kind)]
 
+    def splitk(self, spec, dgrad, N, H, W):
+        return self.e.splitk_ws(spec, dgrad, N, H, W)
+
 
 class AVEngine:
     """Two trunks + the hard-way head on one device."""
@@ -213,10 +216,41 @@ class AVEngine:
         self._alloc(flat.flat.device)
         # run the audio trunk on a second HIP stream, concurrently with the vision trunk (forward and
         # backward): the two trunks are independent until the head, and their kernels fill each
-        # other's wave-quantisation tails.  The fused step turns it off for world > 1 (the bucketed
-        # all-reduce orders its collectives on one stream).
+        # other's wave-quantisation tails.  With world > 1 the backward keeps both trunks concurrent
+        # in two segments (layer4+3, then layer2..stem) joined at the boundary, where on_boundary(tags)
+        # issues the bucketed all-reduce of the finished gradients (train.py).
         self.concurrent = os.environ.get("AVT_CONCURRENT", "1") != "0"
         self._side = None
+        self.wgrad_streams = int(os.environ.get("AVT_WGRAD_STREAMS", "0"))
+        self._wstreams = None
+        # split-K for the short layer3/4 grids (a few clips per GPU): per call site a persistent ticket
+        # array (the kernel leaves it zero) and a partial-tile buffer per call; AVT_SPLITK=0: off
+        self.splitk = os.environ.get("AVT_SPLITK", "0") != "0"
+        self._splitk_cnt: Dict = {}
+
+    def splitk_ws(self, spec, dgrad: bool, N: int, H: int, W: int):
+        """(part, cnt) for a split-K conv call (avt_conv2d_splitk_plan), or None: no split for the shape,
+        split-K off, or (first use) inside a graph capture -- the tickets are allocated zeroed outside
+        capture (the engine runs an eager step before capturing)."""
+        if not self.splitk or spec.k != 3 or spec.stride != 1 or spec.is_stem:
+            return None
+        key = (spec.name, dgrad, N, H, W)
+        ent = self._splitk_cnt.get(key)
+        if ent is None:
+            import ctypes
+            nf, nc = ctypes.c_longlong(0), ctypes.c_int(0)
+            call("avt_conv2d_splitk_plan", N, H, W, spec.cin, spec.cout, 3, 3, 1, 1, int(dgrad), ctypes.byref(nf),
+                 ctypes.byref(nc))
+            if nc.value == 0 or torch.cuda.is_current_stream_capturing():
+                if nc.value == 0:
+                    self._splitk_cnt[key] = (0, None)
+                return None
+            ent = self._splitk_cnt[key] = (nf.value, torch.zeros(nc.value, device=self.flat.flat.device,
+                                                                  dtype=torch.int32))
+        nf, cnt = ent
+        if cnt is None:
+            return None
+        return torch.empty(nf, device=cnt.device, dtype=torch.float32), cnt
 
     def _side_stream(self):
         if self._side is None:
@@ -437,14 +471,17 @@ class AVEngine:
         return gv, gan
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
-                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None):
+                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None, on_trunk_hi=None):
         """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).
         dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141); dA/dPos/dNeg:
         of the returned maps.  The two trunks' backward runs concurrently (audio on the side stream) in
         two segments: layer4+layer3 of both, then layer2..stem of both.  on_boundary(tags) is called
         with ("imgnet.hi", "audnet.hi") between the segments and ("imgnet.lo", "audnet.lo") at the end
         -- on the current stream, after the side stream has joined it, so a gradient all-reduce issued
-        there sees those buckets final (train.py overlaps them with the second segment)."""
+        there sees those buckets final (train.py overlaps them with the second segment).
+        on_trunk_hi(trunk) (without on_boundary): called on each trunk's stream once its layer4+layer3
+        launches are issued; work forked from there (and from trunk.wgrad_stream) sees that trunk's
+        '<prefix>hi' gradients final (train.py starts Adam on them while the rest runs)."""
         gv, gan = self.head_backward(tape, dlogits, dwA, dA=dA, dPos=dPos, dNeg=dNeg)
         a = tape["a"]
         B, C = tape["B"], tape["C"]
@@ -465,19 +502,43 @@ class AVEngine:
 
         def chain(tr, tp, first):
             g, pm = yield from first
+            if on_trunk_hi is not None:  # on the trunk's stream: its layer3+4 launches are all issued
+                on_trunk_hi(tr)
             yield from lo(tr, tp, g, pm)
+
+        wstreams = self._wgrad_streams()
+        img.wgrad_stream, aud.wgrad_stream = wstreams
+
+        def join():
+            img.join_wgrad()
+            aud.join_wgrad()
 
         try:
             img_hi = img.backward_blocks_iter(ti, gv, self.store, hi, len(img.blocks))
             if seg:  # segment 1: layer4+layer3 of both trunks; boundary; segment 2: the rest
                 (ga, pa), (gv, pv) = self._interleave(audio_hi(), img_hi)
+                join()
                 on_boundary((img.prefix + "hi", aud.prefix + "hi"))
                 self._interleave(lo(aud, ta, ga, pa), lo(img, ti, gv, pv))
+                join()
                 on_boundary((img.prefix + "lo", aud.prefix + "lo"))
             else:
                 self._interleave(chain(aud, ta, audio_hi()), chain(img, ti, img_hi))
+                join()
         finally:
+            img.wgrad_stream = aud.wgrad_stream = None
             self.store.grads = None
+
+    def _wgrad_streams(self):
+        """Streams the trunks' weight-gradient launches fork onto in backward (Trunk.wgrad_stream):
+        AVT_WGRAD_STREAMS=2 one per trunk, 1 one shared, 0 none (wgrad inline in the dgrad chain)."""
+        n = self.wgrad_streams if self.concurrent else 0
+        if n <= 0:
+            return None, None
+        if self._wstreams is None:
+            dev = self.flat.flat.device
+            self._wstreams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+        return (self._wstreams[0], self._wstreams[1 if n >= 2 else 0])
 
 
 class TrunkEngine(AVEngine):

@@ -127,6 +127,17 @@ class FlatAdam:
         call("avt_adam_step_dev", P(self.flat.flat), P(gflat), P(self.exp_avg), P(self.exp_avg_sq),
              self.flat.n_train, grad_scale, P(self._hyper), P(self.t_dev), P(self._coef), stream_ptr())
 
+    # step() in parts: prep() once per step (advances the step counter), then apply() over regions that
+    # together cover [0, n_train) exactly once -- the same update, element for element
+    def prep(self):
+        call("avt_adam_prep_dev", P(self._hyper), P(self.t_dev), P(self._coef), stream_ptr())
+
+    def apply(self, gflat: torch.Tensor, lo: int, hi: int, grad_scale: float = 1.0):
+        if lo % 4 or (hi % 4 and hi != self.flat.n_train) or not 0 <= lo <= hi <= self.flat.n_train:
+            raise ValueError(f"FlatAdam.apply: region [{lo}, {hi}) is not 16-byte aligned inside the flat buffer")
+        call("avt_adam_apply_dev", P(self.flat.flat[lo:]), P(gflat[lo:]), P(self.exp_avg[lo:]),
+             P(self.exp_avg_sq[lo:]), hi - lo, grad_scale, P(self._coef), stream_ptr())
+
 
 class FlatMultiStepLR:
     """torch.optim.lr_scheduler.MultiStepLR (train_hardway_1frame.py:118: milestones [60,100,150,180],

@@ -132,6 +132,10 @@ class Store:
         """Zeroed fp64 accumulator for a BN ('fwd': avt_bn_acc_doubles(C); 'bwd': bn_bwd workspace)."""
         ...
 
+    def splitk(self, spec: "ConvSpec", dgrad: bool, N: int, H: int, W: int):
+        """(part, cnt) split-K workspace of this conv call (avt_conv2d_splitk_plan), or None."""
+        return None
+
 
 def _bn_finalize(c_out, acc, rows, bn: BNSpec, store: Store, training: bool, momentum=0.1, eps=1e-5, rep: int = 1):
     """BN statistics -> (scale, shift, mean, invstd) [4, C]; train mode also updates the running
@@ -212,9 +216,14 @@ class Trunk:
         y = torch.empty(N, Pq, Qq, spec.cout, device=x.device, dtype=torch.bfloat16)
         acc = store.stat_acc(bn, "fwd") if training else None
         wf, _ = store.packed(spec)
+        ws = store.splitk(spec, False, N, H, W)
         ev = ConvProfiler.begin()
-        call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
-             spec.stride, spec.pad, spec.kg, stream_ptr())
+        if ws is not None:
+            call("avt_conv2d_fwd_ws", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, spec.kg, P(ws[0]), P(ws[1]), stream_ptr())
+        else:
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, spec.kg, stream_ptr())
         ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + wf.numel() + y.numel()))
         stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, momentum=self.bn_momentum, rep=self.bn_rep)
@@ -321,7 +330,33 @@ class Trunk:
              P(store.grad(bn.prefix + ".bias")), P(gc), P(ws), rows, bn.c, stream_ptr())
         return gc
 
+    # wgrad off the critical path: with a stream set (AVEngine.backward, AVT_WGRAD_STREAMS) every
+    # weight-gradient launch forks onto it from the trunk's stream -- the dgrad -> BN-backward chain
+    # does not wait for them, and their grids fill the CUs the chain's short launches leave idle.
+    # join_wgrad() orders them before the caller's next use of the gradients.
+    wgrad_stream: Optional[torch.cuda.Stream] = None
+
+    def join_wgrad(self):
+        if self.wgrad_stream is not None:
+            torch.cuda.current_stream().wait_stream(self.wgrad_stream)
+        # operands of the forked launches stay referenced until their stream has been joined (the
+        # caching allocator may hand a freed block to the next allocation of its stream at once)
+        self._wgrad_keep = []
+
     def _wgrad(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
+        ws = self.wgrad_stream
+        if ws is None:
+            self._wgrad_launch(x, gy, N, H, W, spec, store)
+            return
+        ws.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(ws):
+            self._wgrad_launch(x, gy, N, H, W, spec, store)
+        keep = getattr(self, "_wgrad_keep", None)
+        if keep is None:
+            keep = self._wgrad_keep = []
+        keep += [x, gy]
+
+    def _wgrad_launch(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
         dw = store.grad(spec.name)
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
                         spec.stride, spec.pad))
@@ -339,8 +374,12 @@ class Trunk:
         the store (dx = the masked gradient g'; avt_conv2d_dgrad_bn)."""
         _, wt = store.packed(spec)
         gx = add if inplace else torch.empty(N, H, W, spec.cin, device=gy.device, dtype=torch.bfloat16)
+        ws = store.splitk(spec, True, N, H, W) if epi is None else None
         ev = ConvProfiler.begin()
-        if add_mask is not None:  # dx = dgrad + add * mask bits
+        if ws is not None:  # short grid: split-K (add / add_mask as below)
+            call("avt_conv2d_dgrad_ws", P(gy), P(wt), P(gx), P(add), P(add_mask), N, H, W, spec.cin, spec.cout,
+                 spec.k, spec.k, spec.stride, spec.pad, P(ws[0]), P(ws[1]), stream_ptr())
+        elif add_mask is not None:  # dx = dgrad + add * mask bits
             assert epi is None
             call("avt_conv2d_dgrad_mask", P(gy), P(wt), P(gx), P(add), P(add_mask), N, H, W, spec.cin, spec.cout,
                  spec.k, spec.k, spec.stride, spec.pad, stream_ptr())

@@ -127,6 +127,21 @@ int avt_conv2d_dgrad(const void* dy, const void* wt, void* dx, const void* add, 
  * the masked copy of g is never stored.  add must not alias dx. */
 int avt_conv2d_dgrad_mask(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
                           int H, int W, int C, int K, int R, int S, int stride, int pad, void* stream);
+/* Split-K form of the 3x3/s1 fwd / dgrad at short grids (a few clips per GPU: layer3/4 of BASELINE
+ * configs[2]'s 32-clip shard), same results to fp32 summation order.  avt_conv2d_splitk_plan gives
+ * the workspace of one call: part = float[*part_floats] (any contents), cnt = int[*counters] zeroed
+ * once (the kernel leaves it zero; one per concurrently running call); both 0 = no split for this
+ * shape (the _ws calls then behave as avt_conv2d_fwd / avt_conv2d_dgrad[_mask]).  dgrad: 0 fwd, 1 dgrad.
+ * avt_set_halo_splitk(s, blocks): s > 0 forces the split count (largest chunk-count divisor <= s),
+ * 0 plans it as the smallest divisor whose grid reaches `blocks` (0: two per CU). */
+int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int dgrad,
+                           long long* part_floats, int* counters);
+int avt_set_halo_splitk(int ksplit, int target_blocks);
+int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
+                      int R, int S, int stride, int pad, int Kg, float* part, int* cnt, void* stream);
+int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
+                        int H, int W, int C, int K, int R, int S, int stride, int pad, float* part, int* cnt,
+                        void* stream);
 /* avt_conv2d_dgrad with the backward of the BatchNorm (+ReLU) that produced dx's positions fused into
  * its store epilogue (BasicBlock.forward, base_models.py:46-49, 58-67): the result g (after `add`) is
  * masked, g' = g * [y > 0] (y given: the block output) or g * [fma(xc, scale, shift) > 0] (y NULL:
@@ -321,6 +336,12 @@ int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
 #define AVT_ADAM_COEF_FLOATS 8
 int avt_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                       float grad_scale, const float* hyper, int* step, float* coef, void* stream);
+/* avt_adam_step_dev in two parts (same update): prep increments *step and writes coef once per step;
+ * apply updates one region of the flat buffers from coef, so the update of a gradient region the
+ * backward has finished can run while the backward computes the rest (train.py) */
+int avt_adam_prep_dev(const float* hyper, int* step, float* coef, void* stream);
+int avt_adam_apply_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                       float grad_scale, const float* coef, void* stream);
 int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd, void* out_dgrad,
                          void* stream);
 /* two launches (fwd copy, dgrad transpose) for many convs: descs = device array of n records

@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
     ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
+    ap.add_argument("--splitk", default="", help="comma list of avt_set_halo_splitk values (0 = plan) to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -124,6 +125,25 @@ def main():
                                          pad, S()))
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
             call("avt_set_halo_stages", 2, 3)
+        if args.splitk and R == 3 and st == 1:
+            for ks in [int(v) for v in args.splitk.split(",")]:
+                call("avt_set_halo_splitk", ks, 0)
+                for dg in (0, 1):
+                    nf, nc = ctypes.c_longlong(0), ctypes.c_int(0)
+                    call("avt_conv2d_splitk_plan", N, H, W, C, K, 3, 3, 1, 1, dg, ctypes.byref(nf), ctypes.byref(nc))
+                    part = torch.empty(max(1, nf.value), device=dev)
+                    cnt = torch.zeros(max(1, nc.value), device=dev, dtype=torch.int32)
+                    pp, pc = (P(part), P(cnt)) if nc.value else (None, None)
+                    if dg == 0:
+                        ms = timeit(lambda: call("avt_conv2d_fwd_ws", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R,
+                                                 st, pad, kg, pp, pc, S()))
+                        line += f" | sk[{ks}:{nc.value and nf.value // (nc.value * 16384)}] fwd {flops / ms / 1e9:6.0f}"
+                    else:
+                        ms = timeit(lambda: call("avt_conv2d_dgrad_ws", P(dy), P(wt), P(dx), None, None, N, H, W, C,
+                                                 K, R, R, st, pad, pp, pc, S()))
+                        line += f" dgrad {flops / ms / 1e9:6.0f}"
+                    tot[(f"{'dgrad' if dg else 'fwd'}_sk{ks}", 1)] = tot.get((f"{'dgrad' if dg else 'fwd'}_sk{ks}", 1), 0) + ms
+            call("avt_set_halo_splitk", 0, 0)
         if (args.nt64 or args.nt128) and args.halo:
             call("avt_set_halo", 0)  # the tap-gather configs on every shape
         if args.nt64 and K == 64 or args.nt64 and C == 64:
