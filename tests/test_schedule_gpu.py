@@ -22,7 +22,7 @@ def _grads(nws: int, graph: bool, segmented: bool, adam_overlap: bool = True):
     m = m.to(dev).train()
     step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
     step.engine.wgrad_streams = nws
-    step.adam_overlap = step.adam_overlap and adam_overlap
+    step.adam_overlap = adam_overlap  # (world 1 only: the segmented world-2 path below never takes it)
     if segmented:
         step.world, step.overlap = 2, True  # the segmented path; the collectives are no-ops
         step._allreduce_bucket = lambda tags, works: None

@@ -4,8 +4,8 @@
 cd ${GRAFT_REPO_ROOT:-/root/repo}; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests/test_splitk_gpu.py tests/test_schedule_gpu.py tests/test_ddp_gpu.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_sched.log 2>&1; rc=$?
 echo "new tests rc=$rc"; grep -E "passed|failed|Error|\{" gpurun_out/t_sched.log | tail -12; [ $rc -ne 0 ] && exit $rc
-BENCH_ARGS="--batch 32 --steps 30" bash tools/ab3.sh 2 "old:AVT_ADAM_OVERLAP=0 AVT_SPLITK=0" "adam:AVT_SPLITK=0" "split:" "sp256:AVT_SPLITK_BLOCKS=256" "sp1k:AVT_SPLITK_BLOCKS=1024" "ws2:AVT_WGRAD_STREAMS=2" "ws1:AVT_WGRAD_STREAMS=1" "fusebn:AVT_FUSE_BN_BWD=1" || exit 1
-BENCH_ARGS="--steps 20" bash tools/ab3.sh 2 "old:AVT_ADAM_OVERLAP=0 AVT_SPLITK=0" "new:" "ws2:AVT_WGRAD_STREAMS=2" || exit 1
+BENCH_ARGS="--batch 32 --steps 30" bash tools/ab3.sh 2 "old:" "adam:AVT_ADAM_OVERLAP=1" "split:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1" "sp256:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_SPLITK_BLOCKS=256" "sp1k:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_SPLITK_BLOCKS=1024" "ws2:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_WGRAD_STREAMS=2" "ws1:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_WGRAD_STREAMS=1" "fusebn:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_FUSE_BN_BWD=1" || exit 1
+BENCH_ARGS="--steps 20" bash tools/ab3.sh 2 "old:" "new:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1" "ws2:AVT_ADAM_OVERLAP=1 AVT_SPLITK=1 AVT_WGRAD_STREAMS=2" || exit 1
 timeout -k 10 300 python tools/conv_bench.py --batch 32 --variants 1 > gpurun_out/cb32.txt 2>&1 || { tail -5 gpurun_out/cb32.txt; exit 1; }
 grep -v amdgpu gpurun_out/cb32.txt
 timeout -k 10 300 python tools/conv_bench.py --batch 32 --only "3x3" --kinds none --variants 1 --splitk "1,2,4,8" > gpurun_out/cbsk32.txt 2>&1 || { tail -5 gpurun_out/cbsk32.txt; exit 1; }
