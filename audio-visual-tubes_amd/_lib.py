@@ -65,6 +65,7 @@ SIGNATURES = {
     "avt_conv2d_dgrad_mask": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_splitk_plan": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "avt_set_halo_splitk": (_I, [_I, _I]),
+    "avt_set_wgrad_nst": (_I, [_I, _I]),
     "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
@@ -111,6 +112,7 @@ SIGNATURES = {
     "avt_adam_step_dev": (_I, [_P, _P, _P, _P, _L, _F, _P, _P, _P, _P]),
     "avt_adam_prep_dev": (_I, [_P, _P, _P, _P]),
     "avt_adam_apply_dev": (_I, [_P, _P, _P, _P, _L, _F, _P, _P]),
+    "avt_pack_conv_weights_part": (_I, [_P, _I, _L, _I, _P]),
     "avt_pack_conv_weight": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_pack_desc_bytes": (_Z, []),
     "avt_pack_conv_weights_batched": (_I, [_P, _I, _L, _P]),

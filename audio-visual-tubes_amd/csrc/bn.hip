@@ -34,26 +34,30 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// one thread per channel
+// 16 lanes per channel, one per slot: the slot reads (just written by memory-side atomics, so served
+// from memory) are one round trip instead of 16 dependent ones per thread; the lanes' sums meet by
+// shuffles (fixed tree order).  Launch: 16 channels per 256-thread block.
+static_assert(AVT_BN_SLOTS == 16, "the finalize kernels map one lane to each of 16 slots");
+__device__ __forceinline__ double sum16(double v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, float momentum, float eps, float* scale,
                                                           float* shift, float* save_mean, float* save_invstd,
                                                           long long rep) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0, R = 0.0;
-#pragma unroll
-  for (int s = 0; s < AVT_BN_SLOTS; ++s) {
-    double* a = acc + ((size_t)s * C + c) * 3;
-    S += a[0];
-    Q += a[1];
-    R += a[2];
-    a[0] = 0.0;
-    a[1] = 0.0;
-    a[2] = 0.0;
-  }
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
+  if (c >= C) return;  // whole 16-lane groups leave together
+  double* a = acc + ((size_t)s * C + c) * 3;
+  const double S = sum16(a[0]), Q = sum16(a[1]), R = sum16(a[2]);
+  a[0] = 0.0;
+  a[1] = 0.0;
+  a[2] = 0.0;
+  if (s != 0) return;
   const double n = (double)rows;
   const double mean = S / n;
   double m2 = Q + (R - S * mean);
@@ -235,40 +239,38 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   }
 }
 
-// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.
-__device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, double inv_rows,
+// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.  16 lanes per
+// channel, one per slot (as bn_finalize_kernel); lane s of channel c's group.
+__device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, int s, double inv_rows,
                                                     float* dgamma, float* dbeta, float* k1, float* k2) {
-  double a = 0.0, b = 0.0;
-#pragma unroll
-  for (int s = 0; s < AVT_BN_SLOTS; ++s) {
-    double* p = acc + ((size_t)s * C + c) * 2;
-    a += p[0];
-    b += p[1];
-    p[0] = 0.0;
-    p[1] = 0.0;
-  }
+  double* p = acc + ((size_t)s * C + c) * 2;
+  const double a = sum16(p[0]), b = sum16(p[1]);
+  p[0] = 0.0;
+  p[1] = 0.0;
+  if (s != 0) return;
   if (dbeta) dbeta[c] += (float)a;
   if (dgamma) dgamma[c] += (float)b;
   k1[c] = (float)(a * inv_rows);
   k2[c] = (float)(b * inv_rows);
 }
 
+// launch: 16 channels per 256-thread block
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
                                                               float* dgamma, float* dbeta, float* k1, float* k2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < C) bn_bwd_finalize_one(acc, C, c, inv_rows, dgamma, dbeta, k1, k2);
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (c < C) bn_bwd_finalize_one(acc, C, c, threadIdx.x & 15, inv_rows, dgamma, dbeta, k1, k2);
 }
 
-// both BNs of a first block in one launch: threads [0, C) the first, [C, 2C) the second
+// both BNs of a first block in one launch: channel groups [0, C) the first, [C, 2C) the second
 __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(double* __restrict__ acc, double* __restrict__ acc2,
                                                                int C, double inv_rows, float* dgamma, float* dbeta,
                                                                float* k1, float* k2, float* dgamma2, float* dbeta2,
                                                                float* k1b, float* k2b) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
   if (c < C)
-    bn_bwd_finalize_one(acc, C, c, inv_rows, dgamma, dbeta, k1, k2);
+    bn_bwd_finalize_one(acc, C, c, s, inv_rows, dgamma, dbeta, k1, k2);
   else if (c < 2 * C)
-    bn_bwd_finalize_one(acc2, C, c - C, inv_rows, dgamma2, dbeta2, k1b, k2b);
+    bn_bwd_finalize_one(acc2, C, c - C, s, inv_rows, dgamma2, dbeta2, k1b, k2b);
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
@@ -650,7 +652,7 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
                                float* shift, float* save_mean, float* save_invstd, void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }
@@ -665,7 +667,7 @@ extern "C" int avt_bn_finalize_rep(double* acc, long long rows, long long rep, i
                                    void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize_rep: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0 && rep >= 1, "bn_finalize_rep: empty input");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, rep);
   return check_launch("bn_finalize_rep");
 }
@@ -754,7 +756,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.C = C;
   if (t2) {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st, acc, acc2, C, inv_rows,
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 15) / 16), dim3(256), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
     p.mean2 = t2->mean;
@@ -766,7 +768,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   }
@@ -792,7 +794,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
                        rows, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
@@ -815,7 +817,7 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)gm, nullptr,
@@ -837,7 +839,7 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, nullptr, scale,
@@ -881,7 +883,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
                        (long long)N * P * Q, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, acc, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), (size_t)6 * Q * C, st, (const bf16_t*)gy,
                      (const unsigned char*)idx, (const bf16_t*)c, scale, shift, mean, invstd, gamma, k1, k2,

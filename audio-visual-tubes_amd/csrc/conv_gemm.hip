@@ -514,6 +514,7 @@ static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = 1;        // allow the 8-wave 256-wide wgrad tiles
+static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
 static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
                                    // measured 230-320 TFLOP/s vs 450-820 for the tap-gather kernel, see
@@ -651,6 +652,14 @@ extern "C" int avt_set_small_tiles(int waves) {
 
 extern "C" int avt_set_wgrad_tiles(int big) {
   avt::g_wgrad_big = big ? 1 : 0;
+  return AVT_OK;
+}
+
+// TN wgrad ring depth: nst for the 4-wave tiles (4, 6 or 8), nst_big for the 8-wave 256 x 256 tile (3-5)
+extern "C" int avt_set_wgrad_nst(int nst, int nst_big) {
+  AVT_REQUIRE(nst >= 4 && nst <= 8 && nst_big >= 3 && nst_big <= 5, "set_wgrad_nst: nst in 4..8, nst_big in 3..5");
+  avt::g_wgrad_nst = nst;
+  avt::g_wgrad_nst_big = nst_big;
   return AVT_OK;
 }
 
@@ -1272,8 +1281,9 @@ extern "C" int avt_conv3d_fwd(const void* x, const void* wpack, void* y, double*
 struct WgradPlan {
   GemmTNParams p;
   int BM, BN, tiles, splits;
+  int nst;              // LDS ring stages of the pipelined kernel
   bool pipe;            // LDS-DMA pipelined kernel (C % 8 == 0) vs register-staged (stems)
-  size_t slab_bytes;    // splits * K * R*S*C * 4 when split-K partials go through a slab
+  size_t slab_bytes;    // splits * Mg * Ng * 4 when split-K partials go through a slab
 };
 
 static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
@@ -1314,13 +1324,21 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   // the epilogue still writes a BM x BN fp32 tile, so blocks need deeper K ranges than the wave
   // model picks (measured, tools/conv_bench.py: min 24 k-tiles takes the six downsample wgrads from
   // 0.239 to 0.143 ms at B = 128; the 3x3 shapes keep their optimum at 4)
-  const int min_kt = (R * S == 1) ? max(g_wgrad_min_kt, 24) : g_wgrad_min_kt;
+  static const int min_kt_1x1 = getenv("AVT_WGRAD_MIN_KT_1X1") ? atoi(getenv("AVT_WGRAD_MIN_KT_1X1")) : 24;
+  const int min_kt = (R * S == 1) ? max(g_wgrad_min_kt, min_kt_1x1) : g_wgrad_min_kt;
   int splits;
+  const bool big = pl.BM == 256 || pl.BN == 256;
+  // ring depth: 4 stages (4-wave tiles: two blocks per CU at 128 x 128) / 3 (8-wave); a deeper ring
+  // (AVT_WGRAD_NST / AVT_WGRAD_NST_BIG, or avt_set_wgrad_nst) keeps more k-tiles in flight for a
+  // block alone on its CU -- the small-batch regime, where a block's k range is short and its DMA
+  // latency is exposed (one stage = 32 pixels x (BM + BN) bf16)
+  if (g_wgrad_nst < 0) g_wgrad_nst = getenv("AVT_WGRAD_NST") ? atoi(getenv("AVT_WGRAD_NST")) : 4;
+  if (g_wgrad_nst_big < 0) g_wgrad_nst_big = getenv("AVT_WGRAD_NST_BIG") ? atoi(getenv("AVT_WGRAD_NST_BIG")) : 3;
+  pl.nst = big ? g_wgrad_nst_big : g_wgrad_nst;
   if (g_wgrad_blocks > 0) {
     splits = g_wgrad_blocks / pl.tiles;
   } else {
-    const bool big = pl.BM == 256 || pl.BN == 256;
-    int occ = max(1, 163840 / ((big ? 192 : 256) * (pl.BM + pl.BN)));
+    int occ = max(1, 163840 / (pl.nst * 64 * (pl.BM + pl.BN)));
     if (pl.BM == 256 && pl.BN == 256) occ = 1;
     const long long slots = (long long)num_cus() * occ;
     long long best = -1;
@@ -1344,8 +1362,9 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   p.kt_per_split = kps;
   // slab + reduce pass for moderate split counts (measured faster on layer3/4); very deep splits
   // (layer1/2: 100-200 splits of a small output) keep the fp32 atomics, which overlap the compute
+  // (the slab holds whole tiles in register order: splits x Mg x Ng, conv_tn_pipe.h)
   pl.slab_bytes = (pl.pipe && pl.splits > 1 && pl.splits <= g_wgrad_slab_max)
-                      ? (size_t)pl.splits * K * R * S * Creal * sizeof(float)
+                      ? (size_t)pl.splits * p.Mg * p.Ng * sizeof(float)
                       : 0;
   return pl;
 }
@@ -1361,33 +1380,28 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
     pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
     pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
     pp.slab = slab;
-    if constexpr (BM == 256 && BN == 256)
-      hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 3>), dim3(pl.tiles * pl.splits), dim3(512), 0, st, pp);
-    else if constexpr (BM == 256)
-      hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 2, 3>), dim3(pl.tiles * pl.splits), dim3(512), 0, st, pp);
-    else
-      hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 4>), dim3(pl.tiles * pl.splits), dim3(256), 0, st,
-                         pp);
+    const dim3 grid(pl.tiles * pl.splits);
+    if constexpr (BM == 256 && BN == 256) {
+      if (pl.nst >= 5)
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 5>), grid, dim3(512), 0, st, pp);
+      else if (pl.nst == 4)
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 4>), grid, dim3(512), 0, st, pp);
+      else
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 3>), grid, dim3(512), 0, st, pp);
+    } else if constexpr (BM == 256) {
+      hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 2, 3>), grid, dim3(512), 0, st, pp);
+    } else {
+      if (pl.nst >= 8)
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 8>), grid, dim3(256), 0, st, pp);
+      else if (pl.nst >= 6)
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 6>), grid, dim3(256), 0, st, pp);
+      else
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 4>), grid, dim3(256), 0, st, pp);
+    }
     return;
   }
   if constexpr (BM <= 128)
     hipLaunchKernelGGL((gemm_tn_kernel<CVEC, BM, BN>), dim3(pl.tiles, pl.splits), dim3(256), 0, st, p);
-}
-
-__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int splits, long long n,
-                                                                float* __restrict__ dw) {
-  const long long nv = n / 4;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nv; i += (long long)gridDim.x * blockDim.x) {
-    f32x4 a = reinterpret_cast<const f32x4*>(dw)[i];
-    for (int s = 0; s < splits; ++s) a += reinterpret_cast<const f32x4*>(slab + (size_t)s * n)[i];
-    reinterpret_cast<f32x4*>(dw)[i] = a;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-    const long long i = nv * 4 + threadIdx.x;
-    float a = dw[i];
-    for (int s = 0; s < splits; ++s) a += slab[(size_t)s * n + i];
-    dw[i] = a;
-  }
 }
 
 // ---- halo wgrad plan (conv_wgrad_halo.h) ----
@@ -1587,11 +1601,30 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
     if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
   }
   if (slab) {
-    const long long n = (long long)K * R * S * Creal;
-    long long blocks = (n / 4 + 255) / 256;
-    if (blocks > 2048) blocks = 2048;
+    const long long n4 = (long long)pl.p.Mg * pl.p.Ng / 4;
+    long long blocks = (n4 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, slab, pl.splits, n, dw);
+    const int nnt = pl.p.Ng / BN, ldw = R * S * Creal;
+    const dim3 g((unsigned)blocks), b(256);
+    if (BM == 256 && BN == 256)
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<4, 2, 2, 4>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
+    else if (BM == 256)
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<4, 2, 2, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
+    else if (BM == 128 && BN == 128)
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 2, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
+    else if (BM == 128)
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 2, 1>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
+    else if (BN == 128)
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 1, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
+    else
+      hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 1, 1>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
+                         pl.p.Mg, ldw, dw);
   }
   return check_launch("conv2d_wgrad");
 }

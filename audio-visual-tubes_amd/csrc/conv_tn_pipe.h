@@ -90,6 +90,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
   const unsigned rowB = (unsigned)(p.W * p.Cp * 2), pixB = (unsigned)(p.Cp * 2);
   const unsigned imgB = (unsigned)(p.H * p.W * p.Cp * 2);
   const int step_oh = 32 / p.Q, step_ow = 32 - (32 / p.Q) * p.Q;
+  const bool tiny = p.P * p.Q < 32;
   int b_pix[BI], b_oh[BI], b_ow[BI], y_off[BI], x_off[BI];
   unsigned b_nb[BI], cB[BI];
   bool b_colok[BI];
@@ -150,9 +151,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
         b_ow[i] -= p.Q;
         b_oh[i] += 1;
       }
-      while (b_oh[i] >= p.P) {  // next image (more than once only when P*Q < 32)
+      if (b_oh[i] >= p.P) {  // next image (more than once only for images of fewer than 32 pixels)
         b_oh[i] -= p.P;
         b_nb[i] += imgB;
+        if (tiny)
+          while (b_oh[i] >= p.P) {
+            b_oh[i] -= p.P;
+            b_nb[i] += imgB;
+          }
       }
     }
   };
@@ -220,10 +226,24 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
   }
   wait_vmcnt<0>();
 
-  // ---- epilogue: partial tile -> slab (plain stores) or fp32 atomics into DW[k_out][(r,s,c)] ----
+  // ---- epilogue: the partial tile to the slab in register order -- [split][tile][wave][i][j][quarter]
+  //      x 64 lanes x 16 B, one coalesced 1 KiB store per instruction, no per-element address math
+  //      (wgrad_slab_reduce_native_kernel maps it back to DW) -- or fp32 atomics into DW[k_out][(r,s,c)] ----
+  if (pp.slab) {
+    f32x4* dst = reinterpret_cast<f32x4*>(pp.slab) +
+                 ((size_t)(split * ntiles + tile) * NW + wid) * (TM * TN * 4 * 64) + lane;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          dst[((i * TN + j) * 4 + q) * 64] =
+              f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+    return;
+  }
   const int ldw = p.R * p.S * p.Creal;  // Cp == Creal for this kernel
   const int frow = lane & 31, fhalf = lane >> 5;
-  float* dst = pp.slab ? pp.slab + (size_t)split * p.Mg * ldw : p.dw;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int cc = n0 + wn * (BN / WN) + j * 32 + frow;
@@ -233,12 +253,44 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int row = m0 + wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-        if (cok && row < p.Mg) {
-          if (pp.slab)
-            dst[(size_t)row * ldw + cc] = acc[i][j][v];
-          else
-            atomicAdd(dst + (size_t)row * ldw + cc, acc[i][j][v]);
-        }
+        if (cok && row < p.Mg) atomicAdd(p.dw + (size_t)row * ldw + cc, acc[i][j][v]);
       }
+  }
+}
+
+// DW += sum over splits of the register-order partial tiles of conv_tn_pipe_kernel<WM, WN, TM, TN, *>:
+// one thread per (tile, wave, i, j, quarter, lane) float4 -- 16-B coalesced slab reads, and four DW
+// read-modify-writes (rows r0 .. r0+3 of one column; 32 consecutive columns per half-wave)
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_native_kernel(const float* __restrict__ slab, int splits,
+                                                                       int ntiles, int nnt, int Mg, int ldw,
+                                                                       float* __restrict__ dw) {
+  constexpr int NW = WM * WN, BM = WM * TM * 32, BN = WN * TN * 32;
+  constexpr int PER_TILE = NW * TM * TN * 4 * 64;  // float4s per tile
+  const long long total = (long long)ntiles * PER_TILE;
+  const long long split_stride = total;
+  for (long long f = blockIdx.x * (long long)blockDim.x + threadIdx.x; f < total;
+       f += (long long)gridDim.x * blockDim.x) {
+    f32x4 a = reinterpret_cast<const f32x4*>(slab)[f];
+    for (int s = 1; s < splits; ++s) a += reinterpret_cast<const f32x4*>(slab)[f + s * split_stride];
+    const int lane = (int)(f & 63);
+    long long r = f >> 6;
+    const int q = (int)(r & 3);
+    r >>= 2;
+    const int j = (int)(r % TN);
+    r /= TN;
+    const int i = (int)(r % TM);
+    r /= TM;
+    const int wid = (int)(r % NW);
+    const int tile = (int)(r / NW);
+    const int mt = tile / nnt, nt = tile - mt * nnt;
+    const int wm = wid / WN, wn = wid % WN;
+    const int col = nt * BN + wn * (BN / WN) + j * 32 + (lane & 31);
+    const int r0 = mt * BM + wm * (BM / WM) + i * 32 + 8 * q + 4 * (lane >> 5);
+    if (col < ldw) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (r0 + e < Mg) dw[(size_t)(r0 + e) * ldw + col] += a[e];
+    }
   }
 }

@@ -307,26 +307,6 @@ extern "C" int avt_adam_step_dev(float* param, const float* grad, float* exp_avg
   return check_launch("adam_step_dev");
 }
 
-// avt_adam_step_dev in two parts, so that the update of a finished gradient region can run while the
-// backward still computes the rest (train.py, world 1): prep advances the device step counter and
-// writes coef once per step; apply updates one 16-byte-aligned region [param, param + n) from coef.
-extern "C" int avt_adam_prep_dev(const float* hyper, int* step, float* coef, void* stream) {
-  AVT_REQUIRE(hyper && step && coef, "adam_prep_dev: null pointer");
-  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, hyper, coef);
-  return check_launch("adam_prep_dev");
-}
-
-extern "C" int avt_adam_apply_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
-                                  float grad_scale, const float* coef, void* stream) {
-  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq && coef, "adam_apply_dev: null pointer");
-  AVT_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
-              "adam_apply_dev: buffers must be 16-byte aligned");
-  if (n == 0) return AVT_OK;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                     exp_avg_sq, n, grad_scale, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, coef);
-  return check_launch("adam_apply_dev");
-}
-
 extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int Kg, void* out_fwd,
                                     void* out_dgrad, void* stream) {
   AVT_REQUIRE(w, "pack_conv_weight: null pointer");
@@ -358,6 +338,46 @@ extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long
   hipLaunchKernelGGL(pack_dgrad_batched_kernel, dim3((unsigned)tx, n), dim3(256), 0, (hipStream_t)stream,
                      (const PackDesc*)descs);
   return check_launch("pack_conv_weights_batched");
+}
+
+// One of the two launches of avt_pack_conv_weights_batched: which = 1 the fwd images, 2 the dgrad images
+// (the step issues each trunk's fwd pack at the head of its own branch and the dgrad packs, needed
+// only by the backward, behind the shorter trunk's forward)
+extern "C" int avt_pack_conv_weights_part(const void* descs, int n, long long max_elems, int which, void* stream) {
+  AVT_REQUIRE(descs && n > 0 && (which == 1 || which == 2), "pack_conv_weights_part: bad arguments");
+  AVT_REQUIRE(max_elems >= 0 && max_elems < (1ll << 31), "pack_conv_weights_part: max_elems out of range");
+  if (which == 1) {
+    long long bx = (max_elems / 8 + 255) / 256;
+    bx = bx > 256 ? 256 : (bx < 1 ? 1 : bx);
+    hipLaunchKernelGGL(pack_fwd_batched_kernel, dim3((unsigned)bx, n), dim3(256), 0, (hipStream_t)stream,
+                       (const PackDesc*)descs);
+  } else {
+    long long tx = max_elems / 4096 + 1;
+    tx = tx > 512 ? 512 : tx;
+    hipLaunchKernelGGL(pack_dgrad_batched_kernel, dim3((unsigned)tx, n), dim3(256), 0, (hipStream_t)stream,
+                       (const PackDesc*)descs);
+  }
+  return check_launch("pack_conv_weights_part");
+}
+
+// avt_adam_step_dev in two parts: prep advances the device step counter and writes coef once per step;
+// apply updates one 16-byte-aligned region from coef -- the train step updates each trunk's region at
+// the end of that trunk's backward branch (the shorter trunk's update overlaps the longer's backward)
+extern "C" int avt_adam_prep_dev(const float* hyper, int* step, float* coef, void* stream) {
+  AVT_REQUIRE(hyper && step && coef, "adam_prep_dev: null pointer");
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, hyper, coef);
+  return check_launch("adam_prep_dev");
+}
+
+extern "C" int avt_adam_apply_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+                                  float grad_scale, const float* coef, void* stream) {
+  AVT_REQUIRE(param && grad && exp_avg && exp_avg_sq && coef, "adam_apply_dev: null pointer");
+  AVT_REQUIRE(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) % 16 == 0,
+              "adam_apply_dev: buffers must be 16-byte aligned");
+  if (n == 0) return AVT_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, n, grad_scale, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, coef);
+  return check_launch("adam_apply_dev");
 }
 
 extern "C" int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream) {

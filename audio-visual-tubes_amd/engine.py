@@ -221,11 +221,10 @@ class AVEngine:
         # issues the bucketed all-reduce of the finished gradients (train.py).
         self.concurrent = os.environ.get("AVT_CONCURRENT", "1") != "0"
         self._side = None
-        self.wgrad_streams = int(os.environ.get("AVT_WGRAD_STREAMS", "0"))
-        self._wstreams = None
         # split-K for the short layer3/4 grids (a few clips per GPU): per call site a persistent ticket
         # array (the kernel leaves it zero) and a partial-tile buffer per call; AVT_SPLITK=0: off
         self.splitk = os.environ.get("AVT_SPLITK", "0") != "0"
+        self.split_pack = os.environ.get("AVT_SPLIT_PACK", "1") != "0"
         self._splitk_cnt: Dict = {}
 
     def splitk_ws(self, spec, dgrad: bool, N: int, H: int, W: int):
@@ -310,7 +309,9 @@ class AVEngine:
 
         descs = []
         maxel = 0
+        self._pack_parts = {}  # trunk prefix -> (first descriptor, count, max elements)
         for tr in self.trunks2d:
+            first, tmax = len(descs), 0
             for spec in tr.convs():
                 wf = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
                 wt = None if spec.is_stem else torch.empty(spec.cin, spec.k * spec.k * spec.cout, device=dev,
@@ -320,7 +321,9 @@ class AVEngine:
                 rs = spec.k * spec.k
                 descs.append(struct.pack("<QQQiiiiii", w.data_ptr(), wf.data_ptr(), 0 if wt is None else wt.data_ptr(),
                                          spec.cout, rs, spec.cin, spec.cp, spec.kg, 0))
-                maxel = max(maxel, spec.cout * spec.kg + (0 if wt is None else wt.numel()))
+                tmax = max(tmax, spec.cout * spec.kg + (0 if wt is None else wt.numel()))
+            maxel = max(maxel, tmax)
+            self._pack_parts[tr.prefix] = (first, len(descs) - first, tmax)
         assert len(descs[0]) == int(query("avt_pack_desc_bytes"))
         blob = b"".join(descs)
         self._pack_table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
@@ -343,6 +346,12 @@ class AVEngine:
         """fp32 master weights -> bf16 fwd/dgrad operands of every conv (two batched launches)."""
         call("avt_pack_conv_weights_batched", P(self._pack_table), self._pack_n, self._pack_max, stream_ptr())
 
+    def pack_trunk(self, tr: Trunk, which: int):
+        """One trunk's bf16 operands: which = 1 the fwd images, 2 the dgrad images (one launch)."""
+        first, n, mx = self._pack_parts[tr.prefix]
+        off = first * int(query("avt_pack_desc_bytes"))
+        call("avt_pack_conv_weights_part", P(self._pack_table[off:]), n, mx, which, stream_ptr())
+
     # ----------------------------------------------------------------------------- forward
     @staticmethod
     def _to_nhwc(x: torch.Tensor, cp: int) -> torch.Tensor:
@@ -364,7 +373,11 @@ class AVEngine:
         B = image.shape[0]
         if audio.shape[0] != B:
             raise ValueError("avt: image and audio batch sizes differ")
-        self.pack_weights()
+        # split packing (concurrent trunks): each trunk's fwd operands at the head of its own branch, the
+        # dgrad operands (backward only) behind the vision forward, which finishes before the audio one
+        split_pack = self.concurrent and self.split_pack
+        if not split_pack:
+            self.pack_weights()
         if training:
             self.flat.nbt.add_(1)
             self._stat_arena.zero_()  # accumulators are re-zeroed by their finalize; this is belt and braces
@@ -374,6 +387,8 @@ class AVEngine:
         io_v = {} if layer_io else None
 
         def audio_branch():
+            if split_pack:
+                self.pack_trunk(self.aud, 1)
             xa = self._to_nhwc(audio, 1)
             a, tape_a = yield from self.aud.forward_iter(xa, self.store, training, io_a)
             C = a.shape[-1]
@@ -385,8 +400,14 @@ class AVEngine:
             return a, tape_a, an, amax, anorm
 
         def vision_branch():
+            if split_pack:
+                self.pack_trunk(self.img, 1)
             xi = self._to_nhwc(image, 4)
-            return (yield from self.img.forward_iter(xi, self.store, training, io_v))
+            out = yield from self.img.forward_iter(xi, self.store, training, io_v)
+            if split_pack and training:
+                self.pack_trunk(self.img, 2)
+                self.pack_trunk(self.aud, 2)
+            return out
 
         # audio trunk (side stream) || vision trunk (current stream), launches interleaved
         (a, tape_a, an, amax, anorm), (v, tape_i) = self._interleave(audio_branch(), vision_branch())
@@ -471,7 +492,7 @@ class AVEngine:
         return gv, gan
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
-                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None, on_trunk_hi=None):
+                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None, on_trunk_end=None):
         """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).
         dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141); dA/dPos/dNeg:
         of the returned maps.  The two trunks' backward runs concurrently (audio on the side stream) in
@@ -479,9 +500,9 @@ class AVEngine:
         with ("imgnet.hi", "audnet.hi") between the segments and ("imgnet.lo", "audnet.lo") at the end
         -- on the current stream, after the side stream has joined it, so a gradient all-reduce issued
         there sees those buckets final (train.py overlaps them with the second segment).
-        on_trunk_hi(trunk) (without on_boundary): called on each trunk's stream once its layer4+layer3
-        launches are issued; work forked from there (and from trunk.wgrad_stream) sees that trunk's
-        '<prefix>hi' gradients final (train.py starts Adam on them while the rest runs)."""
+        on_trunk_end(trunk) (without on_boundary): called on each trunk's stream behind its last gradient
+        launch -- that trunk's gradients are final there (train.py updates them while the other trunk's
+        backward still runs)."""
         gv, gan = self.head_backward(tape, dlogits, dwA, dA=dA, dPos=dPos, dNeg=dNeg)
         a = tape["a"]
         B, C = tape["B"], tape["C"]
@@ -502,44 +523,21 @@ class AVEngine:
 
         def chain(tr, tp, first):
             g, pm = yield from first
-            if on_trunk_hi is not None:  # on the trunk's stream: its layer3+4 launches are all issued
-                on_trunk_hi(tr)
             yield from lo(tr, tp, g, pm)
-
-        wstreams = self._wgrad_streams()
-        img.wgrad_stream, aud.wgrad_stream = wstreams
-
-        def join():
-            img.join_wgrad()
-            aud.join_wgrad()
+            if on_trunk_end is not None:  # on the trunk's stream, behind its last gradient launch
+                on_trunk_end(tr)
 
         try:
             img_hi = img.backward_blocks_iter(ti, gv, self.store, hi, len(img.blocks))
             if seg:  # segment 1: layer4+layer3 of both trunks; boundary; segment 2: the rest
                 (ga, pa), (gv, pv) = self._interleave(audio_hi(), img_hi)
-                join()
                 on_boundary((img.prefix + "hi", aud.prefix + "hi"))
                 self._interleave(lo(aud, ta, ga, pa), lo(img, ti, gv, pv))
-                join()
                 on_boundary((img.prefix + "lo", aud.prefix + "lo"))
             else:
                 self._interleave(chain(aud, ta, audio_hi()), chain(img, ti, img_hi))
-                join()
         finally:
-            img.wgrad_stream = aud.wgrad_stream = None
             self.store.grads = None
-
-    def _wgrad_streams(self):
-        """Streams the trunks' weight-gradient launches fork onto in backward (Trunk.wgrad_stream):
-        AVT_WGRAD_STREAMS=2 one per trunk, 1 one shared, 0 none (wgrad inline in the dgrad chain)."""
-        n = self.wgrad_streams if self.concurrent else 0
-        if n <= 0:
-            return None, None
-        if self._wstreams is None:
-            dev = self.flat.flat.device
-            self._wstreams = [torch.cuda.Stream(device=dev) for _ in range(2)]
-        return (self._wstreams[0], self._wstreams[1 if n >= 2 else 0])
-
 
 class TrunkEngine(AVEngine):
     """One ResNet-18 trunk called on its own (``model.imgnet(x)`` / a standalone ``resnet18(modal=...)``,

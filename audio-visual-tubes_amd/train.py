@@ -71,13 +71,12 @@ class HardWayTrainStep:
         self._graph_opt = None
         self._seg_graphs = None
         self.buckets = dict(self.engine.grad_buckets())  # boundary tag -> flat gradient region
-        # world 1: Adam on each trunk's layer3+4 region (94 % of the parameters) starts on its own stream
-        # as soon as that trunk's backward has finished those layers, overlapping the rest of the
-        # backward (AVT_ADAM_OVERLAP=0: one Adam launch after the backward)
-        self.adam_overlap = (self.world == 1 and os.environ.get("AVT_ADAM_OVERLAP", "0") != "0"
-                             and type(self)._fwd_bwd is HardWayTrainStep._fwd_bwd
-                             and type(self.engine).backward is AVEngine.backward)
-        self._adam_stream = None
+        # world 1, concurrent trunks: Adam runs per trunk region at the end of that trunk's backward
+        # branch (no extra stream: the shorter trunk's update overlaps the longer trunk's backward), the
+        # rest of the flat buffer after the join (AVT_ADAM_BRANCH=0: one Adam launch after the backward)
+        self.adam_branch = (self.world == 1 and os.environ.get("AVT_ADAM_BRANCH", "1") != "0"
+                            and type(self)._fwd_bwd is HardWayTrainStep._fwd_bwd
+                            and type(self.engine).backward is AVEngine.backward)
 
     def _fwd_bwd(self, *inputs, on_boundary=None) -> torch.Tensor:
         image, audio = inputs
@@ -86,34 +85,29 @@ class HardWayTrainStep:
         self.engine.backward(tape, out["dlogits"], self.grad, on_boundary)
         return out["loss"]
 
+    def _trunk_region(self, tr):
+        spans = [self.buckets[tr.prefix + k] for k in ("hi", "lo")]
+        return min(a for a, _ in spans), max(b for _, b in spans)
+
     def _fwd_bwd_adam(self, image, audio) -> torch.Tensor:
-        """World 1: forward + CE + backward + Adam, the update of each trunk's 'hi' region forked onto
-        the optimizer stream once that region's gradient is final (its trunk stream and wgrad stream),
-        the remaining regions updated after the backward.  The same update as opt.step(grad)."""
+        """World 1: forward + CE + backward + Adam, each trunk's parameters updated on its own branch
+        as soon as its gradients are final; the same update as opt.step(grad) after the backward."""
         self.opt.prep()
         out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
         self.grad.zero_()
-        if self._adam_stream is None:
-            self._adam_stream = torch.cuda.Stream(device=self.grad.device)
-        ast = self._adam_stream
         done = []
 
-        def hi(tr):
-            lo_, hi_ = self.buckets[tr.prefix + "hi"]
-            ast.wait_stream(torch.cuda.current_stream())
-            if tr.wgrad_stream is not None:
-                ast.wait_stream(tr.wgrad_stream)
-            with torch.cuda.stream(ast):
-                self.opt.apply(self.grad, lo_, hi_)
-            done.append((lo_, hi_))
+        def trunk_end(tr):
+            lo, hi = self._trunk_region(tr)
+            self.opt.apply(self.grad, lo, hi)
+            done.append((lo, hi))
 
-        self.engine.backward(tape, out["dlogits"], self.grad, None, on_trunk_hi=hi)
-        torch.cuda.current_stream().wait_stream(ast)
+        self.engine.backward(tape, out["dlogits"], self.grad, None, on_trunk_end=trunk_end)
         pos = 0
-        for lo_, hi_ in sorted(done) + [(self.flat.n_train, self.flat.n_train)]:
-            if lo_ > pos:
-                self.opt.apply(self.grad, pos, lo_)
-            pos = max(pos, hi_)
+        for lo, hi in sorted(done) + [(self.flat.n_train, self.flat.n_train)]:
+            if lo > pos:
+                self.opt.apply(self.grad, pos, lo)
+            pos = max(pos, hi)
         return out["loss"]
 
     def _allreduce_bucket(self, tags, works: list):
@@ -130,7 +124,7 @@ class HardWayTrainStep:
         return self._eager_step(*inputs)
 
     def _eager_step(self, *inputs: torch.Tensor) -> torch.Tensor:
-        if self.world == 1 and self.adam_overlap:
+        if self.world == 1 and self.adam_branch:
             return self._fwd_bwd_adam(*inputs)
         if self.world == 1:
             loss = self._fwd_bwd(*inputs)
@@ -162,7 +156,7 @@ class HardWayTrainStep:
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                if self.adam_overlap:
+                if self.adam_branch:
                     loss = self._fwd_bwd_adam(*inputs)
                 else:
                     loss = self._fwd_bwd(*inputs)

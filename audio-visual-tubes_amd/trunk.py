@@ -330,33 +330,7 @@ class Trunk:
              P(store.grad(bn.prefix + ".bias")), P(gc), P(ws), rows, bn.c, stream_ptr())
         return gc
 
-    # wgrad off the critical path: with a stream set (AVEngine.backward, AVT_WGRAD_STREAMS) every
-    # weight-gradient launch forks onto it from the trunk's stream -- the dgrad -> BN-backward chain
-    # does not wait for them, and their grids fill the CUs the chain's short launches leave idle.
-    # join_wgrad() orders them before the caller's next use of the gradients.
-    wgrad_stream: Optional[torch.cuda.Stream] = None
-
-    def join_wgrad(self):
-        if self.wgrad_stream is not None:
-            torch.cuda.current_stream().wait_stream(self.wgrad_stream)
-        # operands of the forked launches stay referenced until their stream has been joined (the
-        # caching allocator may hand a freed block to the next allocation of its stream at once)
-        self._wgrad_keep = []
-
     def _wgrad(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
-        ws = self.wgrad_stream
-        if ws is None:
-            self._wgrad_launch(x, gy, N, H, W, spec, store)
-            return
-        ws.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(ws):
-            self._wgrad_launch(x, gy, N, H, W, spec, store)
-        keep = getattr(self, "_wgrad_keep", None)
-        if keep is None:
-            keep = self._wgrad_keep = []
-        keep += [x, gy]
-
-    def _wgrad_launch(self, x, gy, N, H, W, spec: ConvSpec, store: Store):
         dw = store.grad(spec.name)
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
                         spec.stride, spec.pad))

@@ -137,6 +137,9 @@ int avt_conv2d_dgrad_mask(const void* dy, const void* wt, void* dx, const void* 
 int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int dgrad,
                            long long* part_floats, int* counters);
 int avt_set_halo_splitk(int ksplit, int target_blocks);
+/* TN wgrad LDS ring depth: nst for the 4-wave tiles (4 default, 6, 8), nst_big for the 8-wave 256 x 256
+ * tile (3 default, 4, 5) -- deeper rings keep more k-tiles in flight for a block alone on its CU */
+int avt_set_wgrad_nst(int nst, int nst_big);
 int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                       int R, int S, int stride, int pad, int Kg, float* part, int* cnt, void* stream);
 int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
@@ -336,9 +339,9 @@ int avt_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
 #define AVT_ADAM_COEF_FLOATS 8
 int avt_adam_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                       float grad_scale, const float* hyper, int* step, float* coef, void* stream);
-/* avt_adam_step_dev in two parts (same update): prep increments *step and writes coef once per step;
- * apply updates one region of the flat buffers from coef, so the update of a gradient region the
- * backward has finished can run while the backward computes the rest (train.py) */
+/* avt_adam_step_dev in two parts (the same update): prep increments *step and writes coef once per
+ * step; apply updates one region of the flat buffers from coef (train.py: each trunk's region at the
+ * end of that trunk's backward branch) */
 int avt_adam_prep_dev(const float* hyper, int* step, float* coef, void* stream);
 int avt_adam_apply_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
                        float grad_scale, const float* coef, void* stream);
@@ -348,6 +351,8 @@ int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, int Cp, int
  * {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad;} (avt_pack_desc_bytes() each) */
 size_t avt_pack_desc_bytes(void);
 int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream);
+/* one of its two launches: which = 1 the fwd images, 2 the dgrad images */
+int avt_pack_conv_weights_part(const void* descs, int n, long long max_elems, int which, void* stream);
 int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, int Cp, void* stream);
 /* x [N][C][T][H][W] fp32 -> y [(N T)][H][W][Cp] bf16: the 'b c t h w -> (b t) c h w' fold of
  * train_hardway.py:130-131 fused with the NHWC/bf16 conversion */

@@ -425,12 +425,16 @@ def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
          S())
 
 
+@pytest.mark.parametrize("nst", [(4, 3), (8, 5), (6, 4)], ids=["ring4", "ring8", "ring6"])
 @pytest.mark.parametrize("big", [1, 0, "halo"])
 @pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wgrad(case, slab, big):
+def test_conv_wgrad(case, slab, big, nst):
     """big: the 256-wide tap-gather tiles (1), 128-wide only (0), or the halo-reuse kernel for the
-    3x3/s1 cases ("halo", off by default; conv_wgrad_halo.h)."""
+    3x3/s1 cases ("halo", off by default; conv_wgrad_halo.h).  nst: ring depth of the 4-wave / 8-wave
+    tap-gather tiles (avt_set_wgrad_nst; the deep rings change the split plan too)."""
+    if big == "halo" and nst != (4, 3):
+        pytest.skip("ring depth does not apply to the halo wgrad")
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
@@ -439,10 +443,12 @@ def test_conv_wgrad(case, slab, big):
     try:
         call("avt_set_wgrad_tiles", 1 if big == "halo" else big)
         call("avt_set_wgrad_halo", int(big == "halo"))
+        call("avt_set_wgrad_nst", *nst)
         wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
     finally:
         call("avt_set_wgrad_tiles", 1)
         call("avt_set_wgrad_halo", 0)
+        call("avt_set_wgrad_nst", 4, 3)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()

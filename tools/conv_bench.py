@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
     ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
     ap.add_argument("--splitk", default="", help="comma list of avt_set_halo_splitk values (0 = plan) to sweep")
+    ap.add_argument("--wgrad-nst", default="4,3", help="';'-separated nst,nst_big pairs of avt_set_wgrad_nst to sweep")
     args = ap.parse_args()
     dev = torch.device("cuda")
     N = args.batch
@@ -190,16 +191,21 @@ def main():
                                 for t in args.wgrad_tiles.split(",")]:
                     call("avt_set_wgrad_halo", hv)
                     call("avt_set_wgrad_tiles", big)
-                    for pol in args.wgrad_policy.split(";"):
-                        tb, mk = (int(s) for s in pol.split(","))
-                        call("avt_set_wgrad_policy", tb, mk)
-                        wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
-                        ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
-                        ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st,
-                                                 pad, P(ws), wsb if args.slab else 0, S()))
-                        line += f" wgrad[h{hv},t{big},{tb},{mk}] {flops / ms / 1e9:6.0f}"
-                        key = f"wgrad_h{hv}_t{big}_{pol}"
-                        tot[(key, v)] = tot.get((key, v), 0) + ms
+                    for nstp in args.wgrad_nst.split(";"):
+                      if nstp != "4,3":  # (the default: also runs on a library without the setter)
+                          call("avt_set_wgrad_nst", *(int(v) for v in nstp.split(",")))
+                      for pol in args.wgrad_policy.split(";"):
+                          tb, mk = (int(s) for s in pol.split(","))
+                          call("avt_set_wgrad_policy", tb, mk)
+                          wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+                          ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
+                          ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st,
+                                                   pad, P(ws), wsb if args.slab else 0, S()))
+                          line += f" wgrad[h{hv},t{big},{tb},{mk},n{nstp}] {flops / ms / 1e9:6.0f}"
+                          key = f"wgrad_h{hv}_t{big}_{pol}_n{nstp}"
+                          tot[(key, v)] = tot.get((key, v), 0) + ms
+                if args.wgrad_nst != "4,3":
+                    call("avt_set_wgrad_nst", 4, 3)
                 call("avt_set_wgrad_policy", 0, 4)
                 call("avt_set_wgrad_tiles", 1)
                 call("avt_set_wgrad_halo", 0)
