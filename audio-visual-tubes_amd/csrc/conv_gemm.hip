@@ -1282,6 +1282,7 @@ struct WgradPlan {
   GemmTNParams p;
   int BM, BN, tiles, splits;
   int nst;              // LDS ring stages of the pipelined kernel
+  int kg;               // wave groups per block splitting its k range (conv_tn_pipe_kernel KG)
   bool pipe;            // LDS-DMA pipelined kernel (C % 8 == 0) vs register-staged (stems)
   size_t slab_bytes;    // splits * Mg * Ng * 4 when split-K partials go through a slab
 };
@@ -1359,6 +1360,17 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   int kps = (nkt + splits - 1) / splits;
   if (kps < min_kt) kps = min_kt;
   pl.splits = (nkt + kps - 1) / kps;
+  // two wave groups per block (AVT_WGRAD_KG, default 2): the pairs of blocks the plan puts on one CU
+  // become one 8-wave block over both k ranges with ONE partial tile -- half the split-K slab bytes
+  // (or atomics) at the same waves per CU; 4-wave tiles on the 4-stage ring (2 x 64 KB of LDS at 128 x 128)
+  static const int kg_env = getenv("AVT_WGRAD_KG") ? atoi(getenv("AVT_WGRAD_KG")) : 2;
+  pl.kg = 1;
+  const int pair_occ = 163840 / (pl.nst * 64 * (pl.BM + pl.BN));  // 4-wave blocks per CU (2 at 128 x 128)
+  if (kg_env >= 2 && pl.pipe && !big && pl.nst == 4 && pair_occ == 2 && pl.splits >= 2) {
+    pl.kg = 2;
+    kps *= 2;
+    pl.splits = (nkt + kps - 1) / kps;
+  }
   p.kt_per_split = kps;
   // slab + reduce pass for moderate split counts (measured faster on layer3/4); very deep splits
   // (layer1/2: 100-200 splits of a small output) keep the fp32 atomics, which overlap the compute
@@ -1391,7 +1403,9 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
     } else if constexpr (BM == 256) {
       hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 2, 3>), grid, dim3(512), 0, st, pp);
     } else {
-      if (pl.nst >= 8)
+      if (pl.kg == 2)
+        hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 4, 2>), grid, dim3(512), 0, st, pp);
+      else if (pl.nst >= 8)
         hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 8>), grid, dim3(256), 0, st, pp);
       else if (pl.nst >= 6)
         hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 6>), grid, dim3(256), 0, st, pp);

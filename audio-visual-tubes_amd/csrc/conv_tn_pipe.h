@@ -41,10 +41,14 @@ __device__ __forceinline__ int tn_swz(int row) {  // chunk XOR for a row of ROWB
   return ROWB >= 256 ? ((row & 3) << 2) : (((row >> 1) & 1) << 2);
 }
 
-// 4 or 8 waves as WM x WN, each wave TM x TN tiles of 32x32 (8 waves need BM, BN >= 128)
-template <int WM, int WN, int TM, int TN, int NST>
-__global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
-  constexpr int NW = WM * WN;
+// 4 or 8 waves as WM x WN, each wave TM x TN tiles of 32x32 (8 waves need BM, BN >= 128).
+// KG = 2: two such wave groups per block split the block's k range in halves, each through its own LDS
+// ring, and meet in LDS at the end -- one partial tile per block instead of two (the split-K slab
+// traffic, which dominates the short-batch wgrads, halves at the same number of waves)
+template <int WM, int WN, int TM, int TN, int NST, int KG = 1>
+__global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
+  constexpr int NW = WM * WN;  // waves per group
+  static_assert(KG == 1 || KG == 2, "one or two k groups");
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   static_assert(BM == 64 || BM == 128 || BM == 256, "BM");
@@ -55,11 +59,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
   static_assert(AI >= 1 && BI >= 1 && AI * A_RPI * NW == 32 && BI * B_RPI * NW == 32, "tile/wave split");
   constexpr int LPT = AI + BI;
   constexpr int A_BYTES = 32 * AROWB, STAGE = 32 * (AROWB + BROWB);
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem_all[KG * NST * STAGE];
   const GemmTNParams& p = pp.p;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wtot = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kgi = KG > 1 ? wtot / NW : 0;  // this wave's k group
+  const int wid = wtot - kgi * NW;
+  char* const smem = smem_all + kgi * (NST * STAGE);  // the group's ring
   const int wm = wid / WN, wn = wid % WN;
   const int nnt = p.Ng / BN;
   const int ntiles = (p.Mg / BM) * nnt;
@@ -70,10 +77,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
   const int mt = tile / nnt, nt = tile - mt * nnt;
   const int m0 = mt * BM, n0 = nt * BN;
   const int nkt_total = (p.Kred + 31) / 32;
-  const int kt_begin = split * p.kt_per_split;
-  const int kt_end = min(nkt_total, kt_begin + p.kt_per_split);
-  if (kt_begin >= kt_end) return;
-  const int nkt = kt_end - kt_begin;
+  const int kb_begin = split * p.kt_per_split;
+  const int kb_end = min(nkt_total, kb_begin + p.kt_per_split);
+  if (kb_begin >= kb_end) return;
+  // this group's half of the block's k range; both groups run `nkt` steps (the shorter one on
+  // out-of-range dummy tiles, which load zeros), so the block-wide barriers pair up
+  const int nkt = (kb_end - kb_begin + KG - 1) / KG;
+  const int kt_begin = kb_begin + kgi * nkt;
+  const int kt_end = min(kb_end, kt_begin + nkt);
 
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)pp.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)pp.x_bytes, 0x00020000);
@@ -225,6 +236,32 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_tn_pipe_kernel(GemmTNPipePa
       for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
   }
   wait_vmcnt<0>();
+  if constexpr (KG > 1) {  // group 1's accumulators into group 0's, through the (now idle) rings
+    __syncthreads();
+    f32x4* xch = reinterpret_cast<f32x4*>(smem_all) + wid * (TM * TN * 4 * 64) + lane;
+    if (kgi == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            xch[((i * TN + j) * 4 + q4) * 64] =
+                f32x4{acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2], acc[i][j][4 * q4 + 3]};
+    }
+    __syncthreads();
+    if (kgi == 1) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const f32x4 o = xch[((i * TN + j) * 4 + q4) * 64];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q4 + e] += o[e];
+        }
+  }
 
   // ---- epilogue: the partial tile to the slab in register order -- [split][tile][wave][i][j][quarter]
   //      x 64 lanes x 16 B, one coalesced 1 KiB store per instruction, no per-element address math
