@@ -1366,7 +1366,8 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   static const int kg_env = getenv("AVT_WGRAD_KG") ? atoi(getenv("AVT_WGRAD_KG")) : 2;
   pl.kg = 1;
   const int pair_occ = 163840 / (pl.nst * 64 * (pl.BM + pl.BN));  // 4-wave blocks per CU (2 at 128 x 128)
-  if (kg_env >= 2 && pl.pipe && !big && pl.nst == 4 && pair_occ == 2 && pl.splits >= 2) {
+  // (3x3 only: the 1x1 shortcuts' deep k ranges lost 25-30 % at B = 128 as pairs)
+  if (kg_env >= 2 && pl.pipe && !big && pl.nst == 4 && pair_occ == 2 && pl.splits >= 2 && R * S > 1) {
     pl.kg = 2;
     kps *= 2;
     pl.splits = (nkt + kps - 1) / kps;

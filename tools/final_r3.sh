@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 evidence run: full GPU tests, smoke, bench (B=128), rocprof kernel stats, PMC HBM traffic
+# Round-3 evidence run: full GPU tests, smoke, bench (B=128), rocprof kernel stats, PMC HBM traffic
 # (two passes), B=32 bench.  Each GPU step has its own limit; the first failure ends the script.
 cd ${GRAFT_REPO_ROOT:-/root/repo}; mkdir -p gpurun_out; export TMPDIR=/tmp
 R=$(pwd)
