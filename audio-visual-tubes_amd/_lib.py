@@ -47,6 +47,7 @@ SIGNATURES = {
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
+    "avt_set_halo8": (_I, [_I]),
     "avt_set_halo_stages": (_I, [_I, _I]),
     "avt_set_c64": (_I, [_I]),
     "avt_set_s2_dgrad_one": (_I, [_I]),

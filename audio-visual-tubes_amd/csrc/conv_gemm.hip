@@ -551,6 +551,17 @@ static int halo_small_nst() {
   if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 3;
   return g_halo_small_nst;
 }
+// the 8-wave 256 x 128 halo tile (one block per CU) in place of the 128 x 128 one where measured faster
+// (tools/conv_bench.py --halo 1,2; B=128): layer4 (K = 4608: V +5..7 %, A +6..7 %; B=32 A +9 %) and GEMMs
+// whose 256-row tiles fit one wave of blocks (vision layer3: +7..11 %); the audio layer3 GEMM
+// (324 tiles, 1.3 waves) loses 13 %.  AVT_HALO8=0 keeps the 128 x 128 tile everywhere.
+static int g_halo8 = -1;
+static bool halo8_pick(const GemmNTParams& p) {
+  if (g_halo8 < 0) g_halo8 = getenv("AVT_HALO8") ? atoi(getenv("AVT_HALO8")) : 1;
+  if (!g_halo8) return false;
+  if (p.IC >= 512) return true;
+  return (long)((p.M + 255) / 256) * (p.Ng / 128) <= num_cus();
+}
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
 static int c64_enabled() {
   if (g_c64 < 0) {
@@ -599,6 +610,11 @@ extern "C" int avt_set_s2_dgrad_one(int on) {
 
 extern "C" int avt_set_halo(int on) {
   avt::g_halo = on < 0 ? 0 : (on > 2 ? 2 : on);
+  return AVT_OK;
+}
+
+extern "C" int avt_set_halo8(int on) {
+  avt::g_halo8 = on < 0 ? -1 : (on ? 1 : 0);
   return AVT_OK;
 }
 
@@ -1003,7 +1019,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     // measured (tools/conv_bench.py): the 4-wave 128 x 128 form at 2 blocks per CU beats the tap
     // gather on layer3/4 (W <= 19: +2..16 %); the 8-wave 256-row forms a patch of the wider layer1/2
     // images needs (1 block per CU) lose to it (-1..-20 %), so those keep the tap-gather kernel
-    if (p.Ng % 128 == 0 && (g_halo == 2 || 128 + 2 * p.OW + 2 > 168)) {
+    if (p.Ng % 128 == 0 && (g_halo == 2 || 128 + 2 * p.OW + 2 > 168 || halo8_pick(p))) {
       if (256 + 2 * p.OW + 2 <= 336)
         launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
       else

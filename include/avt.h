@@ -84,6 +84,10 @@ int avt_set_nt64_config(int cfg);
  * tiles for W <= 19 (layer3/4), 8-wave 256x128 tiles for W <= 79 (layer2); 0: tap-gather kernel everywhere;
  * 2: the 8-wave forms for every width (and 256x64 for K = 64) — an A/B knob */
 int avt_set_halo(int on);
+/* 1 (default; env AVT_HALO8): under avt_set_halo(1), layer3/4 shapes also take the 8-wave 256x128 halo
+ * tile where it measured faster (C >= 512, or 256-row tiles fitting one wave of blocks); 0: the 4-wave
+ * 128x128 tile for every W <= 19 shape; -1: back to the environment default — an A/B knob */
+int avt_set_halo8(int on);
 /* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
  * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */

@@ -193,8 +193,9 @@ def test_halo_matches_gather(case):
     dy = _rand_act(N, H, W, K, 43).to(DEV)
     outs = []
     try:
-        for halo in (0, 1, 2):
+        for halo, halo8 in ((0, 1), (1, 0), (1, 1), (2, 1)):
             call("avt_set_halo", halo)
+            call("avt_set_halo8", halo8)
             y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
             acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
             call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
@@ -204,8 +205,10 @@ def test_halo_matches_gather(case):
             outs.append((y.float(), dx.float(), acc.view(-1, K, 3).sum(0)))
     finally:
         call("avt_set_halo", 1)
+        call("avt_set_halo8", -1)
     (y0, dx0, a0) = outs[0]
-    for y1, dx1, a1 in outs[1:]:  # default halo forms (W <= 19) and the 8-wave A/B forms (W <= 79)
+    # 4-wave 128x128 and 8-wave 256x128 halo forms for W <= 19 (avt_set_halo8), the 8-wave forms for W <= 79
+    for y1, dx1, a1 in outs[1:]:
         assert rel_err(y1, y0) < 1e-2 and rel_err(dx1, dx0) < 1e-2
         assert (y1 - y0).abs().gt(0).float().mean().item() < 0.1  # mostly bit-equal after bf16 rounding
         torch.testing.assert_close(a1[:, 0], a0[:, 0], rtol=1e-4, atol=1e-2)
@@ -223,6 +226,7 @@ def test_halo_stages_bitwise_equal(case):
     w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
     wf, wt = pack(w, C, R * R * C)
     dy = _rand_act(N, H, W, K, 53).to(DEV)
+    call("avt_set_halo8", 0)  # the ring-depth knob applies to the 4-wave 128 x 128 tile
     try:
         for small in (0, -1):
             call("avt_set_small_tiles", small)
@@ -242,6 +246,7 @@ def test_halo_stages_bitwise_equal(case):
     finally:
         call("avt_set_halo_stages", 2, 3)
         call("avt_set_small_tiles", 1)
+        call("avt_set_halo8", -1)
 
 
 @pytest.mark.parametrize("N,H,W", [(3, 56, 56), (2, 65, 75), (21, 56, 56), (1, 7, 95)])
