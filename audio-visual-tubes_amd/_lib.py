@@ -38,6 +38,12 @@ class BnBwdTarget(ctypes.Structure):
                 ("gc", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
 
 
+class BnStat(ctypes.Structure):
+    """avt_bn_stat (include/avt.h): one train-mode BatchNorm's statistics for avt_bn_apply_fin."""
+    _fields_ = [("acc", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
@@ -70,6 +76,8 @@ SIGNATURES = {
     "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
+    "avt_bn_apply_fin": (_I, [_P, ctypes.POINTER(BnStat), _P, ctypes.POINTER(BnStat), _P, _P, _L, _L, _I, _I, _F, _F,
+                              _P]),
     "avt_bn_bwd_mask": (_I, [_P, _P, ctypes.POINTER(BnBwdTarget), ctypes.POINTER(BnBwdTarget), _L, _I, _P]),
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),

@@ -18,7 +18,11 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define AVT_OK 0
 #define AVT_EINVAL -1
 #define AVT_EHIP -2
-#define AVT_BN_SLOTS 16  // spread of the fp64 BN statistic accumulators (atomic contention)
+// spread of the fp64 BN statistic accumulators (atomic contention); a multiple of 16.  64 measured -1 %
+// at B=32 and B=128 against 16 (tools/build_variant.sh libavt_base.so -DAVT_BN_SLOTS=..., tools/r3_slots.sh)
+#ifndef AVT_BN_SLOTS
+#define AVT_BN_SLOTS 16
+#endif
 
 namespace avt {
 
@@ -55,6 +59,19 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   float t = 0.f;
   for (int i = 0; i < nw; ++i) t += red[i];
   return t;
+}
+
+// Timing diagnostics only (tools/launch_cost.sh): AVT_DIAG_SKIP bit mask of launches to leave out, so
+// that a step's cost of a launch class can be read off a same-box A/B; results are WRONG when set.
+// 1: forward bn_finalize, 2: backward bn finalize, 4: wgrad slab reduce.  Only launches recorded into a
+// graph are left out: the eager steps before the capture leave valid statistics behind, so the replayed
+// kernels see realistic data (MFMA clocks depend on the operand values).
+inline bool diag_skip(int bit, hipStream_t st) {
+  static int v = -1;
+  if (v < 0) v = getenv("AVT_DIAG_SKIP") ? atoi(getenv("AVT_DIAG_SKIP")) : 0;
+  if (!(v & bit)) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
 
 }  // namespace avt

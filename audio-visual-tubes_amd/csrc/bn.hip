@@ -34,14 +34,32 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// 16 lanes per channel, one per slot: the slot reads (just written by memory-side atomics, so served
-// from memory) are one round trip instead of 16 dependent ones per thread; the lanes' sums meet by
-// shuffles (fixed tree order).  Launch: 16 channels per 256-thread block.
-static_assert(AVT_BN_SLOTS == 16, "the finalize kernels map one lane to each of 16 slots");
+// 16 lanes per channel, lane s owning slots s, s+16, s+32, ... (summed in that order): the slot reads
+// (just written by memory-side atomics, so served from memory) are AVT_BN_SLOTS/16 independent loads
+// per lane instead of a dependent chain; the lanes' sums meet by shuffles (fixed tree order).  Launch:
+// 16 channels per 256-thread block.
+static_assert(AVT_BN_SLOTS % 16 == 0, "the finalize kernels spread the slots over 16 lanes");
+constexpr int kSlotsPerLane = AVT_BN_SLOTS / 16;
 __device__ __forceinline__ double sum16(double v) {
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
   return v;
+}
+// lane s's share of element j of an accumulator [slots][C][W] at channel c (slot stride C*W doubles)
+template <int W>
+__device__ __forceinline__ double lane_slots(const double* __restrict__ acc, int C, int c, int s, int j) {
+  const double* p = acc + ((size_t)s * C + c) * W + j;
+  double v = p[0];
+#pragma unroll
+  for (int k = 1; k < kSlotsPerLane; ++k) v += p[(size_t)k * 16 * C * W];
+  return v;
+}
+template <int W>
+__device__ __forceinline__ void lane_slots_zero(double* __restrict__ acc, int C, int c, int s) {
+#pragma unroll
+  for (int k = 0; k < kSlotsPerLane; ++k)
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[((size_t)(s + 16 * k) * C + c) * W + j] = 0.0;
 }
 
 __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
@@ -52,11 +70,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ a
                                                           long long rep) {
   const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
   if (c >= C) return;  // whole 16-lane groups leave together
-  double* a = acc + ((size_t)s * C + c) * 3;
-  const double S = sum16(a[0]), Q = sum16(a[1]), R = sum16(a[2]);
-  a[0] = 0.0;
-  a[1] = 0.0;
-  a[2] = 0.0;
+  const double S = sum16(lane_slots<3>(acc, C, c, s, 0)), Q = sum16(lane_slots<3>(acc, C, c, s, 1)),
+               R = sum16(lane_slots<3>(acc, C, c, s, 2));
+  lane_slots_zero<3>(acc, C, c, s);
   if (s != 0) return;
   const double n = (double)rows;
   const double mean = S / n;
@@ -133,6 +149,115 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     const u32x4 o = pack8(f);
     reinterpret_cast<u32x4*>(out)[i] = o;
     if (mk) mk[i] = (unsigned char)pos_bits8(o);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bn_finalize + bn_apply in one launch (avt_bn_apply_fin).  A separate finalize is a dependent launch
+// between the conv and the apply: with the other trunk's long-running conv blocks holding every
+// CU's registers, each such launch waits for a CU (measured: leaving the 40 forward finalize launches
+// out of the graph saves ~1.0 ms of a 10 ms B=128 step and 0.23 ms of the B=32 one).
+// Block b owns channel group g = b % G (64 channels) over pixel chunk b / G: its prologue merges the
+// slots of those 64 channels (4 lanes per channel doing the work of 4 of bn_finalize_kernel's 16, the
+// same fp64 add order -> bitwise the same scale/shift) and the group's first block writes
+// stats [4][C] and the running statistics.  The accumulators are left as they are: the caller zeroes
+// them before the next accumulation (one memset per trunk and forward; a last-block ticket re-zeroing
+// them here serialised ~4096 atomics on one address: +40 us per launch).
+struct BnStatArgs {
+  double* acc;  // [16][C][3] (avt_bn_acc_doubles)
+  const float* gamma;
+  const float* beta;
+  float* rmean;  // null: no running-stat update
+  float* rvar;
+  float* stats;  // [4][C]: scale, shift, mean, invstd
+};
+struct ApplyFinArgs {
+  const bf16_t* x;
+  const bf16_t* res;  // null: no residual
+  bf16_t* out;
+  unsigned char* mk;  // null: no mask bits
+  BnStatArgs bn, bnr;  // bnr.acc null: the residual is added as is
+  long long rows, rep;
+  int C, G, relu, nblk;
+  float momentum, eps;
+};
+
+__device__ __forceinline__ void fin_group(const BnStatArgs& b, int C, int g, long long rows, long long rep,
+                                          float momentum, float eps, bool write, float* sc, float* sh) {
+  const int t = threadIdx.x, cl = t >> 2, q = t & 3, c = g * 64 + cl;
+  double v[4][3];  // the shares of lanes q, q+4, q+8, q+12 of bn_finalize_kernel's 16
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[k][j] = lane_slots<3>(b.acc, C, c, q + 4 * k, j);
+  double r[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    // lane q holds slots q, q+4, q+8, q+12: (v_q + v_q+8) + (v_q+4 + v_q+12), then lanes ^2, ^1 -- the
+    // order of sum16's xor 8, 4, 2, 1 tree
+    double s = (v[0][j] + v[2][j]) + (v[1][j] + v[3][j]);
+    s += __shfl_xor(s, 2, 4);
+    s += __shfl_xor(s, 1, 4);
+    r[j] = s;
+  }
+  if (q != 0) return;
+  const double n = (double)rows;
+  const double mean = r[0] / n;
+  double m2 = r[1] + (r[2] - r[0] * mean);
+  if (m2 < 0.0) m2 = 0.0;
+  const float var = (float)(m2 / n);
+  const float inv = rsqrtf(var + eps);
+  const float s_ = b.gamma[c] * inv;
+  const float h_ = b.beta[c] - (float)mean * s_;
+  sc[cl] = s_;
+  sh[cl] = h_;
+  if (!write) return;
+  b.stats[c] = s_;
+  b.stats[C + c] = h_;
+  b.stats[2 * C + c] = (float)mean;
+  b.stats[3 * C + c] = inv;
+  if (b.rmean) {
+    const double nl = n * (double)rep;
+    const float unb = nl > 1.0 ? (float)(m2 * (double)rep / (nl - 1.0)) : var;
+    b.rmean[c] = (1.f - momentum) * b.rmean[c] + momentum * (float)mean;
+    b.rvar[c] = (1.f - momentum) * b.rvar[c] + momentum * unb;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_fin_kernel(ApplyFinArgs a) {
+  __shared__ float sc[64], sh[64], rsc[64], rsh[64];
+  const int C = a.C, g = blockIdx.x % a.G, pb = blockIdx.x / a.G, npb = a.nblk / a.G;
+  const bool first = pb == 0;
+  fin_group(a.bn, C, g, a.rows, a.rep, a.momentum, a.eps, first, sc, sh);
+  if (a.bnr.acc) fin_group(a.bnr, C, g, a.rows, a.rep, a.momentum, a.eps, first, rsc, rsh);
+  __syncthreads();
+  // 8 lanes per pixel (64 channels), 32 pixels per block pass
+  const int lane8 = threadIdx.x & 7, cl0 = lane8 * 8;
+  const int cv = C / 8;
+  for (long long p = (long long)pb * 32 + (threadIdx.x >> 3); p < a.rows; p += (long long)npb * 32) {
+    const long long i = p * cv + g * 8 + lane8;
+    float f[8];
+    unpack8(reinterpret_cast<const u32x4*>(a.x)[i], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[cl0 + e], sh[cl0 + e]);
+    if (a.res) {
+      float rr[8];
+      unpack8(reinterpret_cast<const u32x4*>(a.res)[i], rr);
+      if (a.bnr.acc) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += rr[e] * rsc[cl0 + e] + rsh[cl0 + e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] += rr[e];
+      }
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+    }
+    const u32x4 o = pack8(f);
+    reinterpret_cast<u32x4*>(a.out)[i] = o;
+    if (a.mk) a.mk[i] = (unsigned char)pos_bits8(o);
   }
 }
 
@@ -240,13 +365,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 }
 
 // dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.  16 lanes per
-// channel, one per slot (as bn_finalize_kernel); lane s of channel c's group.
+// channel (as bn_finalize_kernel); lane s of channel c's group.
 __device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, int s, double inv_rows,
                                                     float* dgamma, float* dbeta, float* k1, float* k2) {
-  double* p = acc + ((size_t)s * C + c) * 2;
-  const double a = sum16(p[0]), b = sum16(p[1]);
-  p[0] = 0.0;
-  p[1] = 0.0;
+  const double a = sum16(lane_slots<2>(acc, C, c, s, 0)), b = sum16(lane_slots<2>(acc, C, c, s, 1));
+  lane_slots_zero<2>(acc, C, c, s);
   if (s != 0) return;
   if (dbeta) dbeta[c] += (float)a;
   if (dgamma) dgamma[c] += (float)b;
@@ -647,12 +770,57 @@ using namespace avt;
 
 extern "C" size_t avt_bn_acc_doubles(int C) { return (size_t)AVT_BN_SLOTS * C * 3; }
 
+static bool bn_stat_args(const avt_bn_stat* s, int C, BnStatArgs* o) {
+  if (!s) return true;
+  if (!s->acc || !s->gamma || !s->beta || !s->stats || ((uintptr_t)s->acc & 7)) return false;
+  if ((s->running_mean == nullptr) != (s->running_var == nullptr)) return false;
+  o->acc = s->acc;
+  o->gamma = s->gamma;
+  o->beta = s->beta;
+  o->rmean = s->running_mean;
+  o->rvar = s->running_var;
+  o->stats = s->stats;
+  (void)C;
+  return true;
+}
+
+extern "C" int avt_bn_apply_fin(const void* x, const avt_bn_stat* bn, const void* residual, const avt_bn_stat* bn_res,
+                                void* out, void* mask, long long rows, long long rep, int C, int relu, float momentum,
+                                float eps, void* stream) {
+  AVT_REQUIRE(x && bn && out, "bn_apply_fin: null pointer");
+  AVT_REQUIRE(C % 64 == 0 && C <= 2048, "bn_apply_fin: C=%d must be a multiple of 64", C);
+  AVT_REQUIRE(rows > 0 && rep >= 1, "bn_apply_fin: empty input");
+  AVT_REQUIRE(!bn_res || residual, "bn_apply_fin: bn_res without a residual");
+  AVT_REQUIRE(!mask || relu, "bn_apply_fin: mask needs relu");
+  ApplyFinArgs a{};
+  AVT_REQUIRE(bn_stat_args(bn, C, &a.bn) && bn_stat_args(bn_res, C, &a.bnr),
+              "bn_apply_fin: bad avt_bn_stat (null acc/gamma/beta/stats, misaligned acc, or one running stat)");
+  a.x = (const bf16_t*)x;
+  a.res = (const bf16_t*)residual;
+  a.out = (bf16_t*)out;
+  a.mk = (unsigned char*)mask;
+  a.rows = rows;
+  a.rep = rep;
+  a.C = C;
+  a.G = C / 64;
+  a.relu = relu ? 1 : 0;
+  a.momentum = momentum;
+  a.eps = eps;
+  // ~one 256-vector pass per block, at most 1024 blocks (each block's prologue reads 24 KiB of slots)
+  long long pbs = (rows * C / 8 + 255) / 256 / a.G;
+  if (pbs > 1024 / a.G) pbs = 1024 / a.G;
+  if (pbs < 1) pbs = 1;
+  a.nblk = (int)(pbs * a.G);
+  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(a.nblk), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("bn_apply_fin");
+}
+
 extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta,
                                float* running_mean, float* running_var, float momentum, float eps, float* scale,
                                float* shift, float* save_mean, float* save_invstd, void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }
@@ -667,7 +835,7 @@ extern "C" int avt_bn_finalize_rep(double* acc, long long rows, long long rep, i
                                    void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize_rep: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0 && rep >= 1, "bn_finalize_rep: empty input");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, rep);
   return check_launch("bn_finalize_rep");
 }
@@ -756,7 +924,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.C = C;
   if (t2) {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 15) / 16), dim3(256), 0, st, acc, acc2, C, inv_rows,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 15) / 16), dim3(256), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
     p.mean2 = t2->mean;
@@ -768,7 +936,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   }
@@ -794,7 +962,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
                        rows, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
@@ -817,7 +985,7 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)gm, nullptr,
@@ -839,7 +1007,7 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, nullptr, scale,
@@ -883,7 +1051,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
                        (long long)N * P * Q, C, st);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), (size_t)6 * Q * C, st, (const bf16_t*)gy,
                      (const unsigned char*)idx, (const bf16_t*)c, scale, shift, mean, invstd, gamma, k1, k2,

@@ -1631,7 +1631,7 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
   } else {
     if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
   }
-  if (slab) {
+  if (slab && !diag_skip(4, st)) {
     const long long n4 = (long long)pl.p.Mg * pl.p.Ng / 4;
     long long blocks = (n4 + 255) / 256;
     if (blocks > 4096) blocks = 4096;

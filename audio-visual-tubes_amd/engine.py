@@ -196,6 +196,13 @@ class _EngineStore(Store):
     def stat_acc(self, bn, kind):
         return self.e.stat_views[(bn.prefix, kind)]
 
+    def zero_stats(self, trunk):
+        z = self.e._stat_trunk.get(trunk.prefix)
+        if z is None:
+            return False
+        z.zero_()
+        return True
+
     def splitk(self, spec, dgrad, N, H, W):
         return self.e.splitk_ws(spec, dgrad, N, H, W)
 
@@ -331,15 +338,19 @@ class AVEngine:
         # BN accumulators: per BN 'fwd' [slots][C][3] f64 and 'bwd' [slots][C][2] f64 + k1/k2 (2C f32)
         slots = int(query("avt_bn_slots"))
         offs, total = {}, 0
+        spans = {}  # trunk prefix -> its accumulators' contiguous region of the arena
         for tr in self.bn_trunks:
+            first = total
             for bn in tr.bns():
-                n_f = slots * bn.c * 3
+                n_f = int(query("avt_bn_acc_doubles", bn.c))  # [slots][C][3]
                 n_b = slots * bn.c * 2 + bn.c  # + 2C floats == C doubles
                 offs[(bn.prefix, "fwd")] = (total, n_f)
                 offs[(bn.prefix, "bwd")] = (total + n_f, n_b)
                 total += n_f + n_b
+            spans[tr.prefix] = (first, total)
         self._stat_arena = torch.zeros(total, device=dev, dtype=torch.float64)
         self.stat_views = {k: self._stat_arena[o:o + n] for k, (o, n) in offs.items()}
+        self._stat_trunk = {p: self._stat_arena[a:b] for p, (a, b) in spans.items()}
 
     # ----------------------------------------------------------------------------- weights
     def pack_weights(self):
@@ -362,9 +373,11 @@ class AVEngine:
         return y
 
     def forward(self, image: torch.Tensor, audio: torch.Tensor, training: bool, with_ce: bool = False,
-                ce_scale: float = 1.0, layer_io: bool = False):
+                ce_scale: float = 1.0, layer_io: bool = False, vision_pre=None):
         """layer_io: also return each trunk's layer4 input/output ("v_in"/"v", "a_in"/"a", NHWC bf16)
-        for forward hooks registered on imgnet.layer4 / audnet.layer4 (test.py:63)."""
+        for forward hooks registered on imgnet.layer4 / audnet.layer4 (test.py:63).  vision_pre():
+        launches issued at the head of the vision trunk's branch (ordered before the head, concurrent
+        with the audio trunk)."""
         if not image.is_cuda or not audio.is_cuda:
             raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
         if image.shape[1] != 3 or audio.shape[1] != 1:
@@ -378,9 +391,9 @@ class AVEngine:
         split_pack = self.concurrent and self.split_pack
         if not split_pack:
             self.pack_weights()
-        if training:
-            self.flat.nbt.add_(1)
-            self._stat_arena.zero_()  # accumulators are re-zeroed by their finalize; this is belt and braces
+        # training: each trunk zeroes its BN accumulators on its own branch (Trunk.forward_iter), the batch
+        # counters and vision_pre() (e.g. the gradient zeroing of the step) run on the vision branch -- the
+        # shorter trunk's slack, not the serial section
         dev = image.device
 
         io_a = {} if layer_io else None
@@ -400,6 +413,10 @@ class AVEngine:
             return a, tape_a, an, amax, anorm
 
         def vision_branch():
+            if training:
+                self.flat.nbt.add_(1)
+            if vision_pre is not None:
+                vision_pre()
             if split_pack:
                 self.pack_trunk(self.img, 1)
             xi = self._to_nhwc(image, 4)

@@ -77,6 +77,8 @@ class HardWayTrainStep:
         self.adam_branch = (self.world == 1 and os.environ.get("AVT_ADAM_BRANCH", "1") != "0"
                             and type(self)._fwd_bwd is HardWayTrainStep._fwd_bwd
                             and type(self.engine).backward is AVEngine.backward)
+        # Adam's step counter and the gradient zeroing on the vision branch (AVT_VISION_PRE=0: serial)
+        self.vision_pre = os.environ.get("AVT_VISION_PRE", "1") != "0"
 
     def _fwd_bwd(self, *inputs, on_boundary=None) -> torch.Tensor:
         image, audio = inputs
@@ -92,9 +94,16 @@ class HardWayTrainStep:
     def _fwd_bwd_adam(self, image, audio) -> torch.Tensor:
         """World 1: forward + CE + backward + Adam, each trunk's parameters updated on its own branch
         as soon as its gradients are final; the same update as opt.step(grad) after the backward."""
-        self.opt.prep()
-        out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
-        self.grad.zero_()
+        def pre():  # on the vision trunk's branch, off the serial section
+            self.opt.prep()
+            self.grad.zero_()
+
+        if self.vision_pre:
+            out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0, vision_pre=pre)
+        else:
+            self.opt.prep()
+            out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0)
+            self.grad.zero_()
         done = []
 
         def trunk_end(tr):

@@ -15,7 +15,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ._lib import BnBwdTarget, DgradBnEpi, call, query
+from ._lib import BnBwdTarget, BnStat, DgradBnEpi, call, query
 
 STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
 # 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
@@ -132,6 +132,11 @@ class Store:
         """Zeroed fp64 accumulator for a BN ('fwd': avt_bn_acc_doubles(C); 'bwd': bn_bwd workspace)."""
         ...
 
+    def zero_stats(self, trunk: "Trunk") -> bool:
+        """Zero all of trunk's BN accumulators (stat_acc) in one launch; False if this store cannot (the
+        trunk then finalizes in separate launches, which re-zero them)."""
+        return False
+
     def splitk(self, spec: "ConvSpec", dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) split-K workspace of this conv call (avt_conv2d_splitk_plan), or None."""
         return None
@@ -172,6 +177,9 @@ class Trunk:
         self.prefix, self.modal = prefix, modal
         self.bn_rep = 1  # >1: each input sample stands for bn_rep identical ones (tube audio de-dup)
         self.bn_momentum = 0.1  # 0.19: two reference forwards over the same batch in one (two-view audio)
+        # train mode: BN finalize inside the apply launch (avt_bn_apply_fin; AVT_BN_FIN=1).  Off by default:
+        # -1 % at B=32 and B=128 against separate finalize launches (tools/r3_binfin.sh)
+        self.bn_fin = os.environ.get("AVT_BN_FIN", "0") == "1"
         if modal == "audio":
             self.stem = ConvSpec(prefix + "conv1_a.weight", 1, 64, 7, 2, 3, 1)
         else:
@@ -211,7 +219,9 @@ class Trunk:
         return out
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool):
+    def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool, finalize: bool = True):
+        """conv + its BN statistics; finalize=False (training): returns the accumulator in place of the
+        stats, for _bn_apply_fin to finalize in the consuming launch."""
         Pq, Qq = conv_out(H, spec.k, spec.stride, spec.pad), conv_out(W, spec.k, spec.stride, spec.pad)
         y = torch.empty(N, Pq, Qq, spec.cout, device=x.device, dtype=torch.bfloat16)
         acc = store.stat_acc(bn, "fwd") if training else None
@@ -226,8 +236,33 @@ class Trunk:
                  spec.stride, spec.pad, spec.kg, stream_ptr())
         ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + wf.numel() + y.numel()))
+        if not finalize:
+            return y, acc, Pq, Qq
         stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, momentum=self.bn_momentum, rep=self.bn_rep)
         return y, stats, Pq, Qq
+
+    def _bn_apply_fin(self, c, acc, bn: BNSpec, store: Store, res=None, res_acc=None, res_bn=None, mask=None,
+                      eps=1e-5):
+        """Train mode: finalize bn (and res_bn) from their accumulators + apply (+residual) + ReLU in one
+        launch (avt_bn_apply_fin); returns (out, stats[4,C], res_stats[4,C] or None)."""
+        C = c.shape[-1]
+        rows = c.numel() // C
+
+        def stat(b, a):
+            st = torch.empty(4, C, device=c.device, dtype=torch.float32)
+            d = BnStat()
+            d.acc, d.stats = a.data_ptr(), st.data_ptr()
+            d.gamma, d.beta = store.param(b.prefix + ".weight").data_ptr(), store.param(b.prefix + ".bias").data_ptr()
+            d.running_mean = store.buffer(b.prefix + ".running_mean").data_ptr()
+            d.running_var = store.buffer(b.prefix + ".running_var").data_ptr()
+            return st, d
+
+        s, d = stat(bn, acc)
+        sr, dr = stat(res_bn, res_acc) if res_bn is not None else (None, None)
+        out = torch.empty_like(c)
+        call("avt_bn_apply_fin", P(c), ctypes.byref(d), P(res), ctypes.byref(dr) if dr is not None else None, P(out),
+             P(mask), rows, self.bn_rep, C, 1, ctypes.c_float(self.bn_momentum), ctypes.c_float(eps), stream_ptr())
+        return out, s, sr
 
     def forward(self, x: torch.Tensor, store: Store, training: bool, io: Optional[Dict] = None):
         """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape).  io (optional) receives
@@ -239,6 +274,8 @@ class Trunk:
         be issued interleaved on two streams (engine._interleave); returns forward()'s result."""
         N, H, W, _ = x.shape
         tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
+        # this trunk's BN accumulators zeroed (one launch): avt_bn_apply_fin leaves its inputs unzeroed
+        zeroed = training and store.zero_stats(self)
         c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
         yield
         # bn1 -> relu -> maxpool fused: the full-resolution relu(bn1(c0)) is never stored
@@ -251,10 +288,31 @@ class Trunk:
         tape.update(c0=c0, st0=st0, idx=idx, carg=carg, H1=H1, W1=W1)
         yield
         cur, Hc, Wc = p0, H2, W2
+        fuse = training and self.bn_fin and zeroed
         for bi, blk in enumerate(self.blocks):
             if io is not None and bi == 6:
                 io["layer4_in"] = cur
             t = {"x": cur, "H": Hc, "W": Wc}
+            if fuse:  # finalize folded into the apply launches (avt_bn_apply_fin)
+                c1, a1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training, False)
+                yield
+                h1, s1, _ = self._bn_apply_fin(c1, a1, blk["bn1"], store)
+                yield
+                c2, a2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training, False)
+                yield
+                om = torch.empty(c2.numel() // 8, device=x.device, dtype=torch.uint8)
+                if blk["down"] is not None:
+                    cd, ad, _, _ = self._conv_bn(cur, N, Hc, Wc, blk["down"], blk["bnd"], store, training, False)
+                    yield
+                    out, s2, sd = self._bn_apply_fin(c2, a2, blk["bn2"], store, cd, ad, blk["bnd"], om)
+                    t.update(cd=cd, sd=sd)
+                else:
+                    out, s2, _ = self._bn_apply_fin(c2, a2, blk["bn2"], store, cur, mask=om)
+                t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, om=om, Ho=Ho, Wo=Wo)
+                tape["blocks"].append(t)
+                yield
+                cur, Hc, Wc = out, Ho, Wo
+                continue
             c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
             yield
             h1 = torch.empty_like(c1)

@@ -64,8 +64,8 @@ int avt_abi_version(void);
 
 /* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
 /* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
- * statistics are accumulated into bn_acc (fp64 [avt_bn_slots()][K][3], zero on entry, consumed and
- * re-zeroed by avt_bn_finalize).
+ * statistics are accumulated into bn_acc (fp64 [avt_bn_slots()][K][3] = avt_bn_acc_doubles(K), zero on
+ * entry, consumed and re-zeroed by avt_bn_finalize; consumed by avt_bn_apply_fin, the caller re-zeroes).
  * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
 int avt_bn_slots(void);
 /* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
@@ -205,6 +205,24 @@ int avt_bn_finalize_rep(double* acc, long long rows, long long rep, int C, const
 /* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
 int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                  const float* rshift, void* out, long long rows, int C, int relu, void* stream);
+/* One train-mode BatchNorm's statistics for avt_bn_apply_fin */
+typedef struct {
+  double* acc;          /* avt_bn_acc_doubles(C) doubles from a conv epilogue (read, NOT re-zeroed) */
+  const float* gamma;   /* [C] */
+  const float* beta;
+  float* running_mean;  /* [C] updated (momentum, unbiased var) if non-NULL */
+  float* running_var;
+  float* stats;         /* out [4][C]: scale, shift, mean, invstd (as avt_bn_finalize) */
+} avt_bn_stat;
+/* avt_bn_finalize (of bn, and of bn_res when non-NULL) + avt_bn_apply[_mask] in one launch:
+ * out = [relu](x*scale+shift + [residual*rscale+rshift | residual]), mask (optional, needs relu) as
+ * avt_bn_apply_mask; scale/shift bitwise equal to avt_bn_finalize's.  rows: accumulated rows (each
+ * standing for `rep` rows of the logical batch, see avt_bn_finalize_rep); C % 64 == 0.  Unlike
+ * avt_bn_finalize it leaves the accumulators as they are: zero them before the next conv accumulates.  The forward of
+ * BasicBlock.bn1+relu and of bn2 (+downsample.1) + residual + relu (base_models.py:46-49, 58-67). */
+int avt_bn_apply_fin(const void* x, const avt_bn_stat* bn, const void* residual, const avt_bn_stat* bn_res, void* out,
+                     void* mask, long long rows, long long rep, int C, int relu, float momentum, float eps,
+                     void* stream);
 /* avt_bn_apply with relu, also writing the ReLU mask of out as bits: mask [rows][C/8] u8, bit e of byte
  * j = out[.][8j+e] > 0 (the stored bf16 value) -- what the backward's relu mask reads instead of out */
 int avt_bn_apply_mask(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,

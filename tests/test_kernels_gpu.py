@@ -102,6 +102,71 @@ def tiles(request):
     call("avt_set_small_tiles", 1)
 
 
+@pytest.mark.parametrize("form", ["bn1", "identity", "down"])
+@pytest.mark.parametrize("N,H,W,C,rep,mom", [(2, 9, 11, 64, 1, 0.1), (3, 14, 14, 256, 1, 0.1),
+                                             (2, 7, 9, 512, 3, 0.19), (1, 5, 3, 128, 1, 0.1)])
+def test_bn_apply_fin_matches_finalize_apply(form, N, H, W, C, rep, mom):
+    """avt_bn_apply_fin (finalize in the apply launch) == avt_bn_finalize[_rep] + avt_bn_apply[_mask], bitwise:
+    output, mask bits, stats [4,C], running statistics.
+    Forms: BasicBlock.bn1 + relu; bn2 + identity residual + relu (+mask); bn2 + downsample.1 BN residual."""
+    from avt_amd._lib import BnStat
+
+    K = C
+    g = torch.Generator().manual_seed(7)
+    x = _rand_act(N, H, W, 64, 1).relu().to(DEV)
+    w = (torch.randn(K, 3, 3, 64, generator=g) * 0.05).float().to(DEV)
+    wf, _ = pack(w, 64, 9 * 64, with_t=False)
+    rows = N * H * W
+
+    def conv_acc():
+        y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+        acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+        call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, 64, K, 3, 3, 1, 1, 9 * 64, S())
+        return y, acc
+
+    def params(seed):
+        gg = torch.Generator().manual_seed(seed)
+        return [(torch.rand(C, generator=gg) + 0.5).to(DEV), (torch.randn(C, generator=gg) * 0.1).to(DEV),
+                (torch.randn(C, generator=gg) * 0.1).to(DEV), (torch.rand(C, generator=gg) + 0.5).to(DEV)]
+
+    c, acc = conv_acc()
+    cd, accd = conv_acc()
+    res = _rand_act(N, H, W, C, 5).to(DEV) if form == "identity" else (cd if form == "down" else None)
+    pr, pd = params(11), params(12)
+    outs = []
+    for fused in (False, True):
+        p = [t.clone() for t in pr]
+        q = [t.clone() for t in pd]
+        a, ad = acc.clone(), accd.clone()
+        out = torch.empty_like(c)
+        mk = torch.empty(rows * C // 8, device=DEV, dtype=torch.uint8) if form != "bn1" else None
+        st, sd = torch.empty(4, C, device=DEV), torch.empty(4, C, device=DEV)
+        if fused:
+            d, dd = BnStat(), BnStat()
+            for s_, acc_, pp, stt in ((d, a, p, st), (dd, ad, q, sd)):
+                s_.acc, s_.gamma, s_.beta = acc_.data_ptr(), pp[0].data_ptr(), pp[1].data_ptr()
+                s_.running_mean, s_.running_var, s_.stats = pp[2].data_ptr(), pp[3].data_ptr(), stt.data_ptr()
+            call("avt_bn_apply_fin", P(c), ctypes.byref(d), P(res), ctypes.byref(dd) if form == "down" else None,
+                 P(out), P(mk), rows, rep, C, 1, ctypes.c_float(mom), ctypes.c_float(1e-5), S())
+        else:
+            for acc_, pp, stt in ((a, p, st), (ad, q, sd)) if form == "down" else ((a, p, st),):
+                call("avt_bn_finalize_rep", P(acc_), rows, rep, C, P(pp[0]), P(pp[1]), P(pp[2]), P(pp[3]),
+                     ctypes.c_float(mom), ctypes.c_float(1e-5), P(stt[0]), P(stt[1]), P(stt[2]), P(stt[3]), S())
+            rs = (P(sd[0]), P(sd[1])) if form == "down" else (None, None)
+            if mk is not None:
+                call("avt_bn_apply_mask", P(c), P(st[0]), P(st[1]), P(res), *rs, P(out), P(mk), rows, C, S())
+            else:
+                call("avt_bn_apply", P(c), P(st[0]), P(st[1]), P(res), *rs, P(out), rows, C, 1, S())
+        torch.cuda.synchronize()
+        if not fused:  # finalize re-zeroes; avt_bn_apply_fin leaves the zeroing to the caller
+            assert a.abs().max().item() == 0.0
+        outs.append((out.view(torch.int16).cpu(), None if mk is None else mk.cpu(), st.cpu(), p[2].cpu(), p[3].cpu(),
+                     sd.cpu() if form == "down" else None, q[2].cpu() if form == "down" else None))
+    for u, v in zip(*outs):
+        if u is not None:
+            assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_and_bn_partials(case, tiles):
     N, H, W, C, K, R, st, pad = case
@@ -476,16 +541,17 @@ def test_wgrad_large_splitk():
 # ------------------------------------------------------------------------------------------ BN
 def _tile_acc(c):
     """The accumulator a conv epilogue would leave: per 128-row tile t, (sum_t, M2_t, sum_t^2/n_t)
-    added into slot t % 16 (fp64)."""
+    added into slot t % avt_bn_slots() (fp64)."""
     rows = c.double().reshape(-1, c.shape[-1])
     C = rows.shape[1]
-    acc = torch.zeros(16, C, 3, dtype=torch.float64)
+    ns = int(query("avt_bn_slots"))
+    acc = torch.zeros(ns, C, 3, dtype=torch.float64)
     for i, t in enumerate(range(0, rows.shape[0], 128)):
         blk = rows[t:t + 128]
         s = blk.sum(0)
-        acc[i % 16, :, 0] += s
-        acc[i % 16, :, 1] += ((blk - blk.mean(0)) ** 2).sum(0)
-        acc[i % 16, :, 2] += s * s / blk.shape[0]
+        acc[i % ns, :, 0] += s
+        acc[i % ns, :, 1] += ((blk - blk.mean(0)) ** 2).sum(0)
+        acc[i % ns, :, 2] += s * s / blk.shape[0]
     return acc.reshape(-1)
 
 
@@ -590,7 +656,7 @@ def test_bn_mask_bits_fwd_bwd(shape, two):
     call("avt_bn_bwd_mask", P(gydev), P(bits), ctypes.byref(t1), ctypes.byref(t2) if two else None, rows, C, S())
     torch.cuda.synchronize()
     for t, xc, s, gamma in ([(t1, cdev, st, gam)] + ([(t2, cddev, st2, gam2)] if two else [])):
-        assert not t.keep[3][: 16 * C * 2 * 8].any()  # accumulator left zeroed
+        assert not t.keep[3][: int(query("avt_bn_slots")) * C * 2 * 8].any()  # accumulator left zeroed
         ws = torch.zeros(int(query("avt_bn_bwd_workspace", rows, C)), device=DEV, dtype=torch.uint8)
         dg, db, gc = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV), torch.empty_like(xc)
         call("avt_bn_bwd", P(gydev), P(y), P(xc), P(s[2]), P(s[3]), P(D(gamma)), P(dg), P(db), P(gc), None, P(ws),
@@ -653,7 +719,7 @@ def test_bn_relu_bwd(shape):
             call("avt_bn_bwd", P(gyd), P(y), P(cd), P(st[2]), P(st[3]), P(gmd), P(dgamma), P(dbeta), P(gc), None,
                  P(ws), rows, C, S())
         torch.cuda.synchronize()
-        assert not ws[: 16 * C * 2 * 8].any()  # accumulator left zeroed
+        assert not ws[: int(query("avt_bn_slots")) * C * 2 * 8].any()  # accumulator left zeroed
         outs.append((gc.float(), dgamma, dbeta))
     # same mask and sums; only fp64 atomic order may move k1/k2 by an ulp (-> a bf16 ulp of gc)
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=8e-3, atol=1e-4)
@@ -705,7 +771,7 @@ def test_stem_fused(shape):
     call("avt_stem_maxpool_bn_relu_bwd", P(D(gy)), P(idx), P(carg), P(cd), P(st[0]), P(st[1]), P(st[2]),
          P(st[3]), P(D(gamma)), P(dgamma), P(dbeta), P(gc), P(ws), N, H, W, C, S())
     torch.cuda.synchronize()
-    assert not ws[: 16 * C * 2 * 8].any()
+    assert not ws[: int(query("avt_bn_slots")) * C * 2 * 8].any()
     cn = c.double().permute(0, 3, 1, 2).requires_grad_(True)
     gm = gamma.double().requires_grad_(True)
     bt = beta.double().requires_grad_(True)
