@@ -61,11 +61,12 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-// Timing diagnostics only (tools/launch_cost.sh): AVT_DIAG_SKIP bit mask of launches to leave out, so
-// that a step's cost of a launch class can be read off a same-box A/B; results are WRONG when set.
-// 1: forward bn_finalize, 2: backward bn finalize, 4: wgrad slab reduce.  Only launches recorded into a
-// graph are left out: the eager steps before the capture leave valid statistics behind, so the replayed
-// kernels see realistic data (MFMA clocks depend on the operand values).
+// Timing diagnostics only (tools/launch_cost.sh): AVT_DIAG_SKIP bit mask of launches to leave out of a
+// captured graph (1: forward bn_finalize, 2: backward bn finalize, 4: wgrad slab reduce); results are WRONG
+// when set.  Caveat, measured: the step's speed depends on the data -- a graph whose BN statistics are
+// never written normalises with uninitialised scale/shift, its activations collapse, and every MFMA
+// kernel runs ~8-10 % faster (power/clock), which reads as a spurious ~1 ms "cost" of the finalize
+// launches at B=128.
 inline bool diag_skip(int bit, hipStream_t st) {
   static int v = -1;
   if (v < 0) v = getenv("AVT_DIAG_SKIP") ? atoi(getenv("AVT_DIAG_SKIP")) : 0;

@@ -820,7 +820,9 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
                                float* shift, float* save_mean, float* save_invstd, void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
-  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  hipStream_t st = (hipStream_t)stream;
+  if (diag_skip(1, st)) return AVT_OK;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }

@@ -146,6 +146,7 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
   // so the count is exact; wave 0's statistics atomics only make its wait stricter); before half 1:
   // nothing.
   int tile = tlo + jb;
+  double st_s = 0.0, st_m2 = 0.0, st_r = 0.0;  // BN partials of this block's tiles (threads < 64)
   issue_half(tile, 0);
   for (int it = 0; tile < thi; tile += nbx, ++it) {
     const int m0 = tile * BM;
@@ -256,10 +257,10 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
           s += (double)red[k * 64 + tid];
           m2 += (double)red[NWAVE * 64 + k * 64 + tid];
         }
-        double* a = p.stats + ((size_t)(tile % AVT_BN_SLOTS) * p.Ng + tid) * 3;
-        atomicAdd(a + 0, s);
-        atomicAdd(a + 1, m2);
-        atomicAdd(a + 2, s * s / (double)rows_valid);
+        // the three terms are additive over tiles: summed per block, one set of atomics after the loop
+        st_s += s;
+        st_m2 += m2;
+        st_r += s * s / (double)rows_valid;
       }
     }
     // bf16 pairs: lanes 2k / 2k+1 hold columns c / c+1 of the same rows; per pair of accumulator
@@ -301,4 +302,12 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
       }
   }
   wait_vmcnt<0>();  // drain (the last iteration issued an all-out-of-range half 0)
+  // fp64 atomics per block, not per 256-row tile (~7x fewer at B=128: a conv's queued memory-side
+  // atomics measured ~13-17 us of a layer-1 conv, tools/fin_probe.py)
+  if (MODE == MODE_FWD && p.stats != nullptr && tid < 64 && tlo + jb < thi) {
+    double* a = p.stats + ((size_t)(blockIdx.x % AVT_BN_SLOTS) * p.Ng + tid) * 3;
+    atomicAdd(a + 0, st_s);
+    atomicAdd(a + 1, st_m2);
+    atomicAdd(a + 2, st_r);
+  }
 }
