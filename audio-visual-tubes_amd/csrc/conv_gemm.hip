@@ -513,7 +513,7 @@ static int g_wgrad_blocks = 0;     // wgrad split-K: 0 = wave model (wgrad_plan)
 static int g_wgrad_min_kt = 4;
 static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
-static int g_wgrad_big = 1;        // allow the 8-wave 256-wide wgrad tiles
+static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
 static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
@@ -1324,6 +1324,7 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   pl.BM = (K % 128 == 0 && Cp % 8 == 0) || (K % 128 == 0 && Cp == 4) ? 128 : 64;
   // 8-wave 256-wide tiles halve the LDS fill bytes per flop where the GEMM is wide enough
   // (layer4: K_out 512, R*S*C >= 2304); split-K supplies the parallelism
+  if (g_wgrad_big < 0) g_wgrad_big = getenv("AVT_WGRAD_BIG") ? atoi(getenv("AVT_WGRAD_BIG")) : 1;
   if (pl.pipe && g_wgrad_big) {
     if (K % 256 == 0 && K >= 512 && pl.BN == 128) pl.BM = 256;  // measured: a loss on layer3 (K_out 256)
     if (ncols >= 2048 && pl.BM == 256) pl.BN = 256;
