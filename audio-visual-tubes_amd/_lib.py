@@ -48,12 +48,17 @@ class BnStat(ctypes.Structure):
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
     "avt_abi_version": (_I, []),
+    "avt_build_flags": (_I, []),
+    "avt_peak_mfma": (_I, [_P, _I, _I, _I, ctypes.c_uint, _P]),
+    "avt_peak_mfma_flops": (_L, [_I, _I, _I]),
+    "avt_copy16": (_I, [_P, _P, _Z, _I, _P]),
     "avt_bn_slots": (_I, []),
     "avt_set_conv_variant": (_I, [_I]),
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
     "avt_set_halo8": (_I, [_I]),
+    "avt_set_halo_mf16": (_I, [_I]),
     "avt_set_halo_stages": (_I, [_I, _I]),
     "avt_set_c64": (_I, [_I]),
     "avt_set_s2_dgrad_one": (_I, [_I]),
@@ -73,8 +78,8 @@ SIGNATURES = {
     "avt_conv2d_splitk_plan": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "avt_set_halo_splitk": (_I, [_I, _I]),
     "avt_set_wgrad_nst": (_I, [_I, _I]),
-    "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
-    "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
+    "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
     "avt_bn_apply_fin": (_I, [_P, ctypes.POINTER(BnStat), _P, ctypes.POINTER(BnStat), _P, _P, _L, _L, _I, _I, _F, _F,
                               _P]),

@@ -551,6 +551,12 @@ static int halo_small_nst() {
   if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 3;
   return g_halo_small_nst;
 }
+// halo fwd/dgrad on v_mfma_f32_16x16x32_bf16 tiles (conv_halo.h MF16) instead of 32x32x16: -1 = env AVT_HALO_MF16
+static int g_halo_mf16 = -1;
+static int halo_mf16() {
+  if (g_halo_mf16 < 0) g_halo_mf16 = getenv("AVT_HALO_MF16") ? atoi(getenv("AVT_HALO_MF16")) : 0;
+  return g_halo_mf16;
+}
 // the 8-wave 256 x 128 halo tile (one block per CU) in place of the 128 x 128 one where measured faster
 // (tools/conv_bench.py --halo 1,2; B=128): layer4 (K = 4608: V +5..7 %, A +6..7 %; B=32 A +9 %) and GEMMs
 // whose 256-row tiles fit one wave of blocks (vision layer3: +7..11 %); the audio layer3 GEMM
@@ -866,10 +872,18 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
                        dim3(WM * WN * 64), 0, st, p, ha);
     return;
   }
-  if (grid > 0 && MODE == MODE_DGRAD && p.bx != nullptr)
+  if (grid <= 0) return;
+  if (halo_mf16()) {
+    if (MODE == MODE_DGRAD && p.bx != nullptr)
+      hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, true, false, true>), dim3(grid),
+                         dim3(WM * WN * 64), 0, st, p, ha);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false, true>), dim3(grid),
+                         dim3(WM * WN * 64), 0, st, p, ha);
+  } else if (MODE == MODE_DGRAD && p.bx != nullptr)
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>), dim3(grid), dim3(WM * WN * 64), 0,
                        st, p, ha);
-  else if (grid > 0)
+  else
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX>), dim3(grid), dim3(WM * WN * 64), 0, st,
                        p, ha);
 }
@@ -899,6 +913,8 @@ static int g_halo_splitk = -1, g_splitk_blocks = -1;
 struct SplitWs {
   float* part;
   int* cnt;
+  long long part_floats;  // sizes the caller allocated (avt_conv2d_splitk_plan at the time of the call)
+  int counters;
 };
 static bool halo_splitk_shape(const GemmNTParams& p) {
   return halo_eligible(p) && conv_variant() == 1 && p.Ng % 128 == 0 && 128 + 2 * p.OW + 2 <= 168 &&
@@ -945,8 +961,12 @@ static void launch_c64(const GemmNTParams& p, hipStream_t st) {
   ca.W = p.OW;
   ca.H = p.OH;
   ca.tiles = (p.M + c64::BM - 1) / c64::BM;
+#ifdef AVT_DIAG  // wrong-results timing diagnostics: the -DAVT_DIAG build only
   static const int dbg = getenv("AVT_C64_DBG") ? atoi(getenv("AVT_C64_DBG")) : 0;
   ca.dbg = dbg;
+#else
+  ca.dbg = 0;
+#endif
   for (int r = 0; r < 3; ++r)
     for (int s = 0; s < 3; ++s) {
       const int t = r * 3 + s;
@@ -992,7 +1012,10 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
   }
   if (CVEC == 8 && ws != nullptr && p.IT == 1 && p.OT == 1) {
     const int ks = halo_splitk(p);
-    if (ks > 1) {
+    const long long tiles = (long long)((p.M + 127) / 128) * (p.Ng / 128);
+    // the plan is re-made at every call from the current knobs: a workspace sized for another plan
+    // (the knobs changed after it was allocated) runs the shape without split-K rather than overrun it
+    if (ks > 1 && tiles * ks * 128 * 128 <= ws->part_floats && tiles <= ws->counters) {
       launch_halo128<MODE>(p, st, ks, ws->part, ws->cnt);
       return;
     }
@@ -1101,6 +1124,12 @@ extern "C" int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, 
   return AVT_OK;
 }
 
+extern "C" int avt_set_halo_mf16(int on) {
+  AVT_REQUIRE(on >= -1 && on <= 1, "set_halo_mf16: -1, 0 or 1");
+  avt::g_halo_mf16 = on;  // -1: back to the environment default
+  return AVT_OK;
+}
+
 extern "C" int avt_set_halo_splitk(int ksplit, int target_blocks) {
   AVT_REQUIRE(ksplit >= 0 && target_blocks >= 0, "set_halo_splitk: bad arguments");
   g_halo_splitk = ksplit;
@@ -1109,9 +1138,10 @@ extern "C" int avt_set_halo_splitk(int ksplit, int target_blocks) {
 }
 
 extern "C" int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W,
-                                 int Cp, int K, int R, int S, int stride, int pad, int Kg, float* part, int* cnt,
-                                 void* stream) {
-  const SplitWs ws{part, cnt};
+                                 int Cp, int K, int R, int S, int stride, int pad, int Kg, float* part,
+                                 long long part_floats, int* cnt, int counters, void* stream) {
+  AVT_REQUIRE(part_floats >= 0 && counters >= 0, "conv2d_fwd_ws: negative workspace size");
+  const SplitWs ws{part, cnt, part_floats, counters};
   return conv2d_fwd_impl(x, wpack, y, bn_acc, N, H, W, Cp, K, R, S, stride, pad, Kg, (part && cnt) ? &ws : nullptr,
                          stream);
 }
@@ -1229,9 +1259,10 @@ static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const voi
 // avt_conv2d_dgrad / avt_conv2d_dgrad_mask (add_mask optional) with a split-K workspace
 extern "C" int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask,
                                    int N, int H, int W, int C, int K, int R, int S, int stride, int pad, float* part,
-                                   int* cnt, void* stream) {
+                                   long long part_floats, int* cnt, int counters, void* stream) {
   AVT_REQUIRE(add_mask == nullptr || (add && add != dx), "conv2d_dgrad_ws: add_mask needs add, not aliasing dx");
-  const SplitWs ws{part, cnt};
+  AVT_REQUIRE(part_floats >= 0 && counters >= 0, "conv2d_dgrad_ws: negative workspace size");
+  const SplitWs ws{part, cnt, part_floats, counters};
   return conv2d_dgrad_impl(dy, wt, dx, add, add_mask, N, H, W, C, K, R, S, stride, pad, nullptr, stream,
                            (part && cnt) ? &ws : nullptr);
 }
@@ -1352,7 +1383,8 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   // latency is exposed (one stage = 32 pixels x (BM + BN) bf16)
   if (g_wgrad_nst < 0) g_wgrad_nst = getenv("AVT_WGRAD_NST") ? atoi(getenv("AVT_WGRAD_NST")) : 4;
   if (g_wgrad_nst_big < 0) g_wgrad_nst_big = getenv("AVT_WGRAD_NST_BIG") ? atoi(getenv("AVT_WGRAD_NST_BIG")) : 3;
-  pl.nst = big ? g_wgrad_nst_big : g_wgrad_nst;
+  // (the 256 x 128 8-wave tile always runs the 3-stage ring, launch_tn: nst_big is the 256 x 256 tile's)
+  pl.nst = (pl.BM == 256 && pl.BN == 256) ? g_wgrad_nst_big : big ? 3 : g_wgrad_nst;
   if (g_wgrad_blocks > 0) {
     splits = g_wgrad_blocks / pl.tiles;
   } else {

@@ -41,7 +41,19 @@ __device__ __forceinline__ f32x4 load_wt16(__amdgpu_buffer_rsrc_t rs, unsigned o
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
 }
 
-// WM x WN waves, each TM x TN 32x32 accumulators: BM = WM*TM*32 rows, BN = WN*TN*32 columns.
+// LDS chunk swizzle of a 128-B row (8 16-B chunks): the 32x32x16 fragment reads (lanes 0-31 one chunk of 32
+// consecutive rows) are conflict-free with chunk ^ ((row >> 1) & 7); the 16x16x32 reads (a 16-lane bank
+// group = rows +0..3 and +12..15 of one chunk and rows +4..11 of the next) with chunk ^ (row & 6) -- for
+// ANY first row, which the tap shifts of the patch make arbitrary (exhaustive check over the 16 offsets)
+template <bool MF16>
+__device__ __forceinline__ int halo_swz(int row) {
+  return MF16 ? (row & 6) : ((row >> 1) & 7);
+}
+
+// WM x WN waves, each TM x TN 32x32 output blocks: BM = WM*TM*32 rows, BN = WN*TN*32 columns.  MF16: each
+// 32x32 block as 2x2 v_mfma_f32_16x16x32_bf16 tiles instead of one v_mfma_f32_32x32x16_bf16 (same cycles
+// per FLOP, same LDS bytes per FLOP; the chip holds a higher clock under the 16x16 shape on random data,
+// MI355X_MICROARCH.md DVFS item 7).
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
 // EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
 // LDS of the main loop (two patch buffers + the weight ring): two blocks per CU when two fit in 160 KB
@@ -50,9 +62,14 @@ constexpr int halo_blocks_per_cu() {
   return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false>
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
+          bool MF16 = false>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
+  static_assert(!(MF16 && SPLIT), "split-K runs the 32x32x16 form");
+  // fragment geometry: FM x FN MFMA tiles of FR rows per wave, KS k-steps of KD per 64-channel tap
+  constexpr int FR = MF16 ? 16 : 32, FM = MF16 ? 2 * TM : TM, FN = MF16 ? 2 * TN : TN;
+  constexpr int KD = MF16 ? 32 : 16;
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int BK = 64, RB = 128, RPI = 8;  // 64 channels = one 128-B row; 8 rows per 1 KiB DMA
@@ -105,22 +122,23 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     const int pr = q * RPI + lrow;
     const int pix = m0 - pre + pr;
     if (q >= PINSTR || pr >= PR || pix < 0 || pix >= p.M) return kOOB;
-    const int lc = pchunk ^ ((pr >> 1) & 7);
+    const int lc = pchunk ^ halo_swz<MF16>(pr);
     return (unsigned)(((long long)pix * p.IC + chunk_c * BK + lc * 8) * 2);
   };
   unsigned b_off[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int row = (wid * BR + i) * RPI + lrow;
-    const int lc = pchunk ^ ((row >> 1) & 7);
+    const int lc = pchunk ^ halo_swz<MF16>(row);
     b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
   }
-  // ---- fragment rows of this lane: rows wm*(BM/WM) + i*32 + (lane & 31); per row a 9-bit tap mask ----
-  const int frow = lane & 31, fhalf = lane >> 5;
-  unsigned fmask[TM];
+  // ---- fragment rows of this lane: rows wm*(BM/WM) + i*FR + (lane % FR); per row a 9-bit tap mask.  The
+  //      lane's k chunk within a k-step: fhalf (32x32x16: lanes 32-63 take k 8..15) or lane >> 4 (16x16x32) ----
+  const int frow = lane & (FR - 1), fhalf = lane / FR;
+  unsigned fmask[FM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int row = wm * (BM / WM) + i * 32 + frow;
+  for (int i = 0; i < FM; ++i) {
+    const int row = wm * (BM / WM) + i * FR + frow;
     const int m = m0 + row;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
@@ -140,20 +158,25 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   //      B: per (column block, k-step) offset in a ring stage.  With the tap loop unrolled the k loop is
   //      ds_read + MFMA (tap, stage and buffer are compile-time; a rolled (chunk, tap) loop spent ~11
   //      other instructions per MFMA) ----
-  unsigned arow[9][TM];
+  // (MF16: the chunk is k-step * 4 + lane >> 4, so a k-step is an XOR of ks << 6)
+  unsigned arow[9][FM];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int pr = wm * (BM / WM) + i * 32 + frow + pre + ha.tap_disp[t];
+    for (int i = 0; i < FM; ++i) {
+      const int pr = wm * (BM / WM) + i * FR + frow + pre + ha.tap_disp[t];
       const bool v = (fmask[i] >> t) & 1u;
-      arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((fhalf ^ ((pr >> 1) & 7)) << 4));
+      arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((fhalf ^ halo_swz<MF16>(pr)) << 4));
     }
-  int boffs[TN][BK / 16];
+  constexpr int KS = BK / KD;
+  int boffs[FN][KS];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+  for (int j = 0; j < FN; ++j)
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) boffs[j][ks] = swz_rb<RB>(wn * (BN / WN) + j * 32 + frow, ks * 2 + fhalf);
+    for (int ks = 0; ks < KS; ++ks) {
+      const int row = wn * (BN / WN) + j * FR + frow;
+      boffs[j][ks] = row * RB + ((((MF16 ? 4 : 2) * ks + fhalf) ^ halo_swz<MF16>(row)) << 4);
+    }
 
   // ---- issue of step (chunk cn, tap tn): weight tile into ring stage (cn*9+tn) % NSTB, and for tn >=
   //      NSTB-1 one piece of chunk cn+1's patch into patch buffer (cn+1) & 1 (which held chunk cn-1, whose
@@ -177,21 +200,27 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     }
   };
 
-  f32x16 acc[TM][TN];
+  // accumulators: AV fp32 per lane per MFMA tile; element v of tile (i, j) is output row acc_row(i, v),
+  // column wn*(BN/WN) + j*FR + frow
+  constexpr int AV = MF16 ? 4 : 16;
+  using acc_t = typename std::conditional<MF16, f32x4, f32x16>::type;
+  auto acc_row = [&](int i, int v) -> int {
+    return wm * (BM / WM) + i * FR + (MF16 ? fhalf * 4 + v : (v & 3) + 8 * (v >> 2) + 4 * fhalf);
+  };
+  acc_t acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+      for (int v = 0; v < AV; ++v) acc[i][j][v] = 0.f;
 
   // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2
   for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, cbase));
 #pragma unroll
   for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
-  constexpr int KS = BK / 16;
-  bf16x8 af[2][TM], bfr[2][TN];
+  bf16x8 af[2][FM], bfr[2][FN];
   for (int c = 0; c < nchunk; ++c) {
     const char* Ab = smem + (c & 1) * ABUF;  // patch buffer of this chunk
 #pragma unroll
@@ -221,10 +250,10 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
         auto load_frags = [&](int ks, int buf) {
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
+          for (int i = 0; i < FM; ++i)
+            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << (MF16 ? 6 : 5))));
 #pragma unroll
-          for (int j = 0; j < TN; ++j) bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
+          for (int j = 0; j < FN; ++j) bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
         };
         load_frags(0, 0);
         {  // the ring stage read at step s-1; every wave has passed that
@@ -240,10 +269,14 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
             __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < FN; ++j) {
+              if constexpr (MF16)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+              else
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+            }
           if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -252,7 +285,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   wait_vmcnt<0>();
   __syncthreads();
 
-  if constexpr (SPLIT) {
+  if constexpr (SPLIT && !MF16) {
     // partial tile in register order: (wave, i, j, quarter) x 64 lanes x 16 B -- 1 KiB per instruction
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(ha.part + (size_t)tile * ha.ksplit * BM * BN), (short)0, (int)(ha.ksplit * BM * BN * 4), 0x00020000);
@@ -304,37 +337,36 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   const int rows_valid = min(BM, p.M - m0);
   if (MODE == MODE_FWD && p.stats != nullptr) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
+    for (int j = 0; j < FN; ++j) {
       float sm = 0.f;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-          if (r < rows_valid) sm += acc[i][j][v];
-        }
-      sm += __shfl_xor(sm, 32, 64);
-      if (lane < 32) red[wm * BN + wn * (BN / WN) + j * 32 + lane] = sm;
+        for (int v = 0; v < AV; ++v)
+          if (acc_row(i, v) < rows_valid) sm += acc[i][j][v];
+#pragma unroll
+      for (int o = FR; o < 64; o <<= 1) sm += __shfl_xor(sm, o, 64);
+      if (lane < FR) red[wm * BN + wn * (BN / WN) + j * FR + lane] = sm;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int cc = wn * (BN / WN) + j * 32 + frow;
+    for (int j = 0; j < FN; ++j) {
+      const int cc = wn * (BN / WN) + j * FR + frow;
       float tot = 0.f;
 #pragma unroll
       for (int k = 0; k < WM; ++k) tot += red[k * BN + cc];
       const float mean = tot / (float)rows_valid;
       float q = 0.f;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        for (int v = 0; v < AV; ++v) {
           const float d = acc[i][j][v] - mean;
-          if (r < rows_valid) q += d * d;
+          if (acc_row(i, v) < rows_valid) q += d * d;
         }
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 32) red[WM * BN + wm * BN + cc] = q;
+#pragma unroll
+      for (int o = FR; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
+      if (lane < FR) red[WM * BN + wm * BN + cc] = q;
     }
     __syncthreads();
     double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
@@ -353,15 +385,11 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   }
   bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int r = wm * (BM / WM) + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
-        const int cc = wn * (BN / WN) + j * 32 + frow;
-        Ct[r * CT_LD + cc] = f2bf(acc[i][j][v]);
-      }
+      for (int v = 0; v < AV; ++v) Ct[acc_row(i, v) * CT_LD + wn * (BN / WN) + j * FR + frow] = f2bf(acc[i][j][v]);
   __syncthreads();
   epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, [&](int r) -> size_t { return (size_t)(m0 + r); },
                         reinterpret_cast<float*>(smem));

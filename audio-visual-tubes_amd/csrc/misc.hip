@@ -261,6 +261,66 @@ static int grid_for(long long n) {
   return (int)b;
 }
 
+// ---- measured peaks (bench.py's roofline denominators, re-measured on the box in the same run) ----
+// Back-to-back bf16 MFMA on register operands holding pseudo-random bf16 values in [-1, 1) (the chip's
+// clock under MFMA load depends on the operand bits: zeros clock ~19 % higher, MI355X_MICROARCH.md DVFS
+// item 1), NACC independent accumulators per wave, one 256-thread block per CU = one wave per SIMD.
+__device__ __forceinline__ unsigned peak_hash(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+template <int SHAPE>  // 0: v_mfma_f32_32x32x16_bf16 (4 accumulators), 1: v_mfma_f32_16x16x32_bf16 (8)
+__global__ __launch_bounds__(256) void peak_mfma_kernel(float* __restrict__ sink, int iters, unsigned seed) {
+  const unsigned g = blockIdx.x * 256u + threadIdx.x;
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // bf16 with a random mantissa and sign, exponent of [0.5, 1)
+    const unsigned ha = peak_hash(seed ^ (g * 16u + j)), hb = peak_hash(~seed ^ (g * 16u + 8u + j));
+    a[j] = __builtin_bit_cast(__bf16, (unsigned short)(0x3f00u | (ha & 0x807fu)));
+    b[j] = __builtin_bit_cast(__bf16, (unsigned short)(0x3f00u | (hb & 0x807fu)));
+  }
+  float s = 0.f;
+  if constexpr (SHAPE == 0) {
+    f32x16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) s += acc[i][v];
+  } else {
+    f32x4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[i][v] = 0.f;
+    for (int it = 0; it < iters; ++it)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) s += acc[i][v];
+  }
+  sink[g] = s;  // keeps the loop live; one vector store per lane
+}
+
+// grid-stride 16-byte copy (the HBM read + write rate a streaming kernel reaches on this box)
+__global__ __launch_bounds__(256) void copy16_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, long long n) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) dst[i] = src[i];
+}
+
 }  // namespace avt
 
 using namespace avt;
@@ -268,6 +328,38 @@ using namespace avt;
 extern "C" const char* avt_last_error(void) { return g_err; }
 
 extern "C" int avt_abi_version(void) { return 1; }
+
+extern "C" int avt_build_flags(void) {
+#ifdef AVT_DIAG
+  return AVT_BUILD_DIAG;
+#else
+  return 0;
+#endif
+}
+
+extern "C" long long avt_peak_mfma_flops(int shape, int blocks, int iters) {
+  if ((shape != 0 && shape != 1) || blocks < 1 || iters < 1) return -1;
+  // 32x32x16: 4 accumulators x 32*32*16*2 FLOP; 16x16x32: 8 x 16*16*32*2 -- per wave and iteration
+  const long long per_wave_iter = shape == 0 ? 4ll * 32768 : 8ll * 16384;
+  return per_wave_iter * iters * blocks * 4;
+}
+
+extern "C" int avt_peak_mfma(float* sink, int shape, int blocks, int iters, unsigned seed, void* stream) {
+  AVT_REQUIRE(sink && (shape == 0 || shape == 1) && blocks >= 1 && iters >= 1, "peak_mfma: bad arguments");
+  if (shape == 0)
+    hipLaunchKernelGGL(peak_mfma_kernel<0>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, sink, iters, seed);
+  else
+    hipLaunchKernelGGL(peak_mfma_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, sink, iters, seed);
+  return check_launch("peak_mfma");
+}
+
+extern "C" int avt_copy16(void* dst, const void* src, size_t bytes, int blocks, void* stream) {
+  AVT_REQUIRE(dst && src && bytes % 16 == 0 && blocks >= 1, "copy16: bad arguments");
+  AVT_REQUIRE(((uintptr_t)dst | (uintptr_t)src) % 16 == 0, "copy16: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(copy16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
+                     (long long)(bytes / 16));
+  return check_launch("copy16");
+}
 
 // torch.optim.Adam (amsgrad=False, maximize=False) with coupled L2 weight decay on one flat segment;
 // grad is multiplied by grad_scale first (1/world for a summed all-reduce).

@@ -240,7 +240,8 @@ class AVEngine:
         capture (the engine runs an eager step before capturing)."""
         if not self.splitk or spec.k != 3 or spec.stride != 1 or spec.is_stem:
             return None
-        key = (spec.name, dgrad, N, H, W)
+        # one ticket array per call site AND stream: two same-shape calls on different streams never share one
+        key = (spec.name, dgrad, N, H, W, torch.cuda.current_stream().cuda_stream)
         ent = self._splitk_cnt.get(key)
         if ent is None:
             import ctypes

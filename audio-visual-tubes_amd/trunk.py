@@ -230,7 +230,7 @@ class Trunk:
         ev = ConvProfiler.begin()
         if ws is not None:
             call("avt_conv2d_fwd_ws", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
-                 spec.stride, spec.pad, spec.kg, P(ws[0]), P(ws[1]), stream_ptr())
+                 spec.stride, spec.pad, spec.kg, P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), stream_ptr())
         else:
             call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, spec.cp, spec.cout, spec.k, spec.k,
                  spec.stride, spec.pad, spec.kg, stream_ptr())
@@ -410,7 +410,7 @@ class Trunk:
         ev = ConvProfiler.begin()
         if ws is not None:  # short grid: split-K (add / add_mask as below)
             call("avt_conv2d_dgrad_ws", P(gy), P(wt), P(gx), P(add), P(add_mask), N, H, W, spec.cin, spec.cout,
-                 spec.k, spec.k, spec.stride, spec.pad, P(ws[0]), P(ws[1]), stream_ptr())
+                 spec.k, spec.k, spec.stride, spec.pad, P(ws[0]), ws[0].numel(), P(ws[1]), ws[1].numel(), stream_ptr())
         elif add_mask is not None:  # dx = dgrad + add * mask bits
             assert epi is None
             call("avt_conv2d_dgrad_mask", P(gy), P(wt), P(gx), P(add), P(add_mask), N, H, W, spec.cin, spec.cout,

@@ -27,9 +27,14 @@ Inputs are synthetic and already resident in HBM when the timed region starts; w
 random-init (no checkpoints).  Prints ONE JSON line on rank 0.  `roofline` is for the dominant
 kernel family (the implicit-GEMM convolutions), measured live with HIP events around every conv
 launch of eager steps run right after the timed region: achieved = algorithmic conv FLOPs / summed
-kernel time; `traffic` = PMC-measured HBM bytes per conv launch from the committed profile of the
-same workload (tools/pmc_traffic.sh).  `cpu_baseline` times the oracle's fp32 PyTorch-CPU
-restatement of the same step on the host cores (rank 0, N=1 only).
+kernel time; `traffic` = PMC-measured HBM bytes per conv launch, measured live by two rocprofv3
+--pmc passes (FETCH_SIZE, WRITE_SIZE) over child runs of the same workload on this build (N=1), else
+taken from profiles/conv_traffic_*.json only if that record names this build's source hash, else null.
+`peak` is the vendor dense bf16 peak; `peak_measured` re-measures it on this box in the same run (an
+MFMA loop on random operands), next to a 16-byte HBM copy (`peaks_measured`), so a slow box can be
+told from a slow build.  Every AVT_* variable is recorded (`avt_env`); the wrong-results diagnostics
+(AVT_DIAG_SKIP, AVT_C64_DBG) and a -DAVT_DIAG build of the library are refused.  `cpu_baseline`
+times the oracle's fp32 PyTorch-CPU restatement of the same step on the host cores (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -62,23 +67,116 @@ def synthetic_inputs(B, device, seed, frames=0):
     return img, spec
 
 
+ALG_BYTES_PER_CLIP = 80.8e6  # each conv's input and output once in fwd, dgrad and wgrad (bf16)
+
+# environment knobs that make the library compute WRONG results (timing diagnostics); a bench run refuses them.
+# Every other AVT_* variable (A/B performance knobs) is recorded in the JSON line.
+WRONG_RESULT_KNOBS = ("AVT_DIAG_SKIP", "AVT_C64_DBG", "AVT_TN_DBG")
+
+
+def check_env():
+    """Refuse wrong-results knobs (before any GPU call); return every AVT_* variable for the record."""
+    bad = [k for k in WRONG_RESULT_KNOBS if os.environ.get(k, "0") not in ("", "0")]
+    if bad:
+        sys.exit(f"bench.py: refusing to run with wrong-results diagnostics set: {', '.join(bad)}")
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("AVT_")}
+
+
 def traffic_file(workload, B):
     tag = {"1frame": "b", "tube": "tube_b", "twoview": "twoview_b"}[workload]
     return os.path.join(REPO, "profiles", f"conv_traffic_{tag}{B}.json")
 
 
-def conv_traffic(path, launches_per_step, B):
-    """HBM bytes per conv launch from the committed PMC summary (tools/pmc_traffic.sh ->
-    tools/traffic_summary.py --json) of this same workload; None if absent or for another batch."""
+def _load_traffic(path, B, lib_hash):
+    """A traffic record (tools/traffic_summary.py) if it is for this batch AND this library's sources."""
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None, None
-    if t.get("per_gpu_batch") != B or launches_per_step <= 0:
-        return None, None
-    per_step = t["conv_read_bytes_per_step"] + t["conv_write_bytes_per_step"]
-    return round(per_step / launches_per_step), os.path.relpath(path, REPO)
+        return None, "absent"
+    if t.get("per_gpu_batch") != B:
+        return None, f"{os.path.relpath(path, REPO)} is for batch {t.get('per_gpu_batch')}"
+    if t.get("lib_source_hash") != lib_hash:
+        return None, f"{os.path.relpath(path, REPO)} is stale (measured on another build of libavt)"
+    return t, os.path.relpath(path, REPO)
+
+
+def live_traffic(args, B, lib_hash, timeout_s=240):
+    """HBM bytes of this build's step from PMC counters, measured now: two rocprofv3 passes (FETCH_SIZE,
+    WRITE_SIZE; they do not fit one pass on gfx950), kernel-trace only, each over a child bench.py running
+    1 warm-up + 1 eager step of the same workload (tools/pmc_traffic.sh's recipe).  The child is started
+    as a subprocess (never exec'd) after this process's own measurements are done."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if exe is None:
+        return None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import traffic_summary as ts
+
+    child = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1", "--warmup", "1", "--no-graph",
+             "--prof-steps", "0", "--no-cpu-baseline", "--traffic", "off", "--no-peaks", "--batch", str(B),
+             "--workload", args.workload, "--frames", str(args.frames)]
+    child += ["--twoview-folded"] if args.twoview_folded else []
+    child += ["--tube-folded"] if args.tube_folded else []
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    with tempfile.TemporaryDirectory(prefix="avt_pmc_") as d:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = [exe, "--pmc", ctr, "--kernel-trace", "--output-format", "csv", "-d", os.path.join(d, ctr),
+                   "-o", "run", "--"] + child
+            try:
+                r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {ctr} timed out"
+            if r.returncode != 0:
+                tail = r.stdout.decode(errors="replace").strip().splitlines()[-1:]
+                return None, f"rocprofv3 --pmc {ctr} failed ({r.returncode}): {tail}"
+        t = ts.summarize(d, 2.0, B, "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over 2 eager steps of this "
+                         "workload (read = 2 x FETCH_SIZE KiB, gfx950 correction; write = WRITE_SIZE KiB)", lib_hash)
+    if t["conv_dispatches_per_step"] <= 0:
+        return None, "PMC passes saw no conv kernels"
+    return t, "live"
+
+
+def measure_peaks(dev, seconds=1.0):
+    """Peaks of THIS box, now (the chip's clock varies 5-12 % across MI355X devices and with the data):
+    bf16 MFMA loops on random register operands (32x32x16 and 16x16x32, one wave per SIMD), and a
+    16-byte HBM copy over 2 x 1 GiB.  HIP events on the launch stream."""
+    from avt_amd._lib import call, query
+
+    st = torch.cuda.current_stream(dev)
+    blocks = torch.cuda.get_device_properties(dev).multi_processor_count
+    sink = torch.empty(blocks * 256, device=dev, dtype=torch.float32)
+    out = {}
+
+    def timed(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(n):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e-3
+
+    for shape, key in ((0, "mfma_32x32x16_bf16"), (1, "mfma_16x16x32_bf16")):
+        iters = 4000
+        launch = lambda: call("avt_peak_mfma", sink.data_ptr(), shape, blocks, iters, 12345, st.cuda_stream)
+        t1 = timed(launch, 2) / 2  # warm-up + calibration
+        iters = max(1000, int(iters * 0.02 / max(t1, 1e-6)))  # ~20 ms launches
+        n = max(3, int(seconds / 0.02))
+        t = timed(launch, n)
+        out[key] = query("avt_peak_mfma_flops", shape, blocks, iters) * n / t / 1e12
+    nbytes = 1 << 30
+    src = torch.ones(nbytes // 4, device=dev, dtype=torch.float32)
+    dst = torch.empty_like(src)
+    cp = lambda: call("avt_copy16", dst.data_ptr(), src.data_ptr(), nbytes, blocks * 8, st.cuda_stream)
+    timed(cp, 2)
+    n = 20
+    out["hbm_copy_tbs"] = 2 * nbytes * n / timed(cp, n) / 1e12  # read + write
+    del src, dst
+    return out
 
 
 def _cores():
@@ -184,7 +282,13 @@ def main():
                     "captured HIP graph of the step")
     ap.add_argument("--prof-steps", type=int, default=2, help="eager steps with HIP events around every conv "
                     "launch after the timed region (roofline)")
+    ap.add_argument("--traffic", choices=["live", "file", "off"], default="live", help="roofline.traffic: live = "
+                    "two rocprofv3 PMC passes over this workload after the measurement (N=1; falls back to file), "
+                    "file = the committed profiles/conv_traffic_*.json if it was measured on this build, off = null")
+    ap.add_argument("--traffic-out", default="", help="write the traffic record (tools/traffic_summary.py format) here")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the in-run MFMA / HBM peak measurement")
     args = ap.parse_args()
+    avt_env = check_env()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -198,10 +302,14 @@ def main():
     dev = torch.device("cuda", local)
 
     import avtubes  # noqa: F401
+    from avt_amd import _lib
     from avt_amd.model import AVENet, FullModel, HardWayArgs
     from avt_amd.train import HardWayTrainStep, TwoViewTrainStep
     from avt_amd.trunk import ConvProfiler
 
+    if _lib.query("avt_build_flags") & 1:  # AVT_BUILD_DIAG
+        sys.exit("bench.py: refusing to run on the -DAVT_DIAG timing-diagnostics build of libavt (wrong results)")
+    lib_hash = _lib.source_hash() if _lib.LOAD_PATH == _lib.LIB_PATH else None
     tube = args.workload == "tube"
     twoview = args.workload == "twoview"
     strong = False
@@ -275,6 +383,7 @@ def main():
         torch.cuda.synchronize()
     step.engine.concurrent = conc
     conv = prof.summary()
+    peaks = None if args.no_peaks else measure_peaks(dev)
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -289,8 +398,24 @@ def main():
         n_launch = sum(v[0] for v in conv.values())
         alg_bytes = sum(v[3] for v in conv.values())
         achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-        traffic, traffic_src = conv_traffic(traffic_file(args.workload, B), n_launch / ps, B)
         conv_tflop_step = fl / ps / 1e12
+        trec, traffic_src = None, "off"
+        if args.traffic == "live" and world == 1 and lib_hash is not None:
+            trec, traffic_src = live_traffic(args, B, lib_hash)
+        if trec is None and args.traffic != "off":
+            why = traffic_src
+            trec, traffic_src = _load_traffic(traffic_file(args.workload, B), B, lib_hash)
+            if trec is None and args.traffic == "live":
+                traffic_src = f"live: {why}; file: {traffic_src}"
+        if trec is not None and args.traffic_out:
+            with open(args.traffic_out, "w") as f:
+                json.dump(trec, f, indent=1)
+        lps = n_launch / ps
+        traffic = None
+        if trec is not None and lps > 0:
+            traffic = round((trec["conv_read_bytes_per_step"] + trec["conv_write_bytes_per_step"]) / lps)
+        step_tflops = conv_tflop_step / (ms_step * 1e-3)
+        peak_meas = peaks["mfma_32x32x16_bf16"] if peaks else None
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -311,6 +436,8 @@ def main():
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per conv launch (PMC FETCH_SIZE/WRITE_SIZE, gfx950-corrected)",
                          "traffic_source": traffic_src,
+                         "peak_measured": round(peak_meas, 1) if peak_meas else None,
+                         "frac_vs_measured": round(achieved / peak_meas, 4) if peak_meas else None,
                          "algorithmic_bytes_per_launch": round(alg_bytes / max(n_launch, 1)),
                          "algorithmic_flops_per_launch": round(fl / max(n_launch, 1)),
                          "launches": n_launch,
@@ -323,8 +450,17 @@ def main():
                 ", audio trunk on a second stream" if step.engine.concurrent else ""),
             # whole step: algorithmic conv FLOPs of one step / step time (head, BN, Adam: < 1 %)
             "step_conv_tflop": round(conv_tflop_step, 4),
-            "step_tflops_per_gpu": round(conv_tflop_step / (ms_step * 1e-3), 2),
-            "step_mfma_frac": round(conv_tflop_step / (ms_step * 1e-3) / MFMA_BF16_PEAK_TFLOPS, 4),
+            "step_tflops_per_gpu": round(step_tflops, 2),
+            "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+            "step_mfma_frac_vs_measured": round(step_tflops / peak_meas, 4) if peak_meas else None,
+            # SURVEY 8(d)'s secondary HBM view: clips/s x 80.8 MB algorithmic bytes per clip / (G x 8 TB/s)
+            "hbm_view_frac": round(value * ALG_BYTES_PER_CLIP / (world * HBM_PEAK_GBS * 1e9), 4)
+            if args.workload == "1frame" else None,
+            "step_hbm_bytes": round(trec["step_bytes"]) if trec else None,
+            "step_hbm_tbs": round(trec["step_bytes"] / (ms_step * 1e-3) / 1e12, 3) if trec else None,
+            "peaks_measured": {k: round(v, 2) for k, v in peaks.items()} if peaks else None,
+            "peak_units": {"mfma_*": "TFLOP/s", "hbm_copy_tbs": "TB/s (read + write)"},
+            "avt_env": avt_env,
             "loss": round(loss_v, 6),
             "cpu_baseline": None,
         }

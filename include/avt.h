@@ -61,6 +61,20 @@ extern "C" {
 
 const char* avt_last_error(void);
 int avt_abi_version(void);
+/* bit mask of how this library was built: AVT_BUILD_DIAG = the timing-diagnostics build (-DAVT_DIAG:
+ * environment knobs that drop launches or loads and give WRONG results); bench.py refuses such a build */
+#define AVT_BUILD_DIAG 1
+int avt_build_flags(void);
+
+/* ---- measured peaks (bench.py's roofline denominators, re-measured in the same run) ---- */
+/* back-to-back bf16 MFMA on pseudo-random register operands, one wave per SIMD (256-thread blocks):
+ * shape 0 = v_mfma_f32_32x32x16_bf16 (4 accumulators), 1 = v_mfma_f32_16x16x32_bf16 (8); sink:
+ * float[blocks*256] (one value per lane, keeps the loop live).  avt_peak_mfma_flops: the FLOPs of one
+ * such launch (-1 on bad arguments). */
+int avt_peak_mfma(float* sink, int shape, int blocks, int iters, unsigned seed, void* stream);
+long long avt_peak_mfma_flops(int shape, int blocks, int iters);
+/* dst = src, 16-byte vector loads/stores in a grid-stride loop of `blocks` 256-thread blocks (bytes % 16 == 0) */
+int avt_copy16(void* dst, const void* src, size_t bytes, int blocks, void* stream);
 
 /* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
 /* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
@@ -71,8 +85,8 @@ int avt_bn_slots(void);
 /* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
-/* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) in 2..3, nst64 (64 x 128
- * small-batch tile) in 2..5; all settings give bitwise-identical results (A/B knob) */
+/* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) and nst64 (64 x 128
+ * small-batch tile) in 2..5 (3 or more: one block per CU); all settings give bitwise-identical results (A/B knob) */
 int avt_set_halo_stages(int nst128, int nst64);
 /* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
  * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
@@ -88,6 +102,9 @@ int avt_set_halo(int on);
  * tile where it measured faster (C >= 512, or 256-row tiles fitting one wave of blocks); 0: the 4-wave
  * 128x128 tile for every W <= 19 shape; -1: back to the environment default — an A/B knob */
 int avt_set_halo8(int on);
+/* 1: the halo fwd/dgrad tiles run on v_mfma_f32_16x16x32_bf16 (2x2 per 32x32 block) instead of 32x32x16;
+ * 0: 32x32x16; -1: the environment default (AVT_HALO_MF16) — an A/B knob (fp32 sums in another order) */
+int avt_set_halo_mf16(int on);
 /* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
  * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */
@@ -144,11 +161,14 @@ int avt_set_halo_splitk(int ksplit, int target_blocks);
 /* TN wgrad LDS ring depth: nst for the 4-wave tiles (4 default, 6, 8), nst_big for the 8-wave 256 x 256
  * tile (3 default, 4, 5) -- deeper rings keep more k-tiles in flight for a block alone on its CU */
 int avt_set_wgrad_nst(int nst, int nst_big);
+/* part_floats / counters: the sizes of part and cnt as allocated; the plan is re-made at every call from the
+ * current knobs, and a call whose plan needs more than the workspace holds runs without split-K. */
 int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
-                      int R, int S, int stride, int pad, int Kg, float* part, int* cnt, void* stream);
+                      int R, int S, int stride, int pad, int Kg, float* part, long long part_floats, int* cnt,
+                      int counters, void* stream);
 int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* add, const void* add_mask, int N,
-                        int H, int W, int C, int K, int R, int S, int stride, int pad, float* part, int* cnt,
-                        void* stream);
+                        int H, int W, int C, int K, int R, int S, int stride, int pad, float* part,
+                        long long part_floats, int* cnt, int counters, void* stream);
 /* avt_conv2d_dgrad with the backward of the BatchNorm (+ReLU) that produced dx's positions fused into
  * its store epilogue (BasicBlock.forward, base_models.py:46-49, 58-67): the result g (after `add`) is
  * masked, g' = g * [y > 0] (y given: the block output) or g * [fma(xc, scale, shift) > 0] (y NULL:

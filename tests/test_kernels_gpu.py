@@ -102,6 +102,14 @@ def tiles(request):
     call("avt_set_small_tiles", 1)
 
 
+@pytest.fixture(params=[0, 1], ids=["mfma32", "mfma16"])
+def mf16(request):
+    """Run the halo fwd/dgrad tiles on 32x32x16 MFMAs, then on 16x16x32 ones (avt_set_halo_mf16)."""
+    call("avt_set_halo_mf16", request.param)
+    yield request.param
+    call("avt_set_halo_mf16", -1)
+
+
 @pytest.mark.parametrize("form", ["bn1", "identity", "down"])
 @pytest.mark.parametrize("N,H,W,C,rep,mom", [(2, 9, 11, 64, 1, 0.1), (3, 14, 14, 256, 1, 0.1),
                                              (2, 7, 9, 512, 3, 0.19), (1, 5, 3, 128, 1, 0.1)])
@@ -168,7 +176,7 @@ def test_bn_apply_fin_matches_finalize_apply(form, N, H, W, C, rep, mom):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_and_bn_partials(case, tiles):
+def test_conv_fwd_and_bn_partials(case, tiles, mf16):
     N, H, W, C, K, R, st, pad = case
     x = _rand_act(N, H, W, C, 1).relu()
     g = torch.Generator().manual_seed(2)
@@ -258,9 +266,10 @@ def test_halo_matches_gather(case):
     dy = _rand_act(N, H, W, K, 43).to(DEV)
     outs = []
     try:
-        for halo, halo8 in ((0, 1), (1, 0), (1, 1), (2, 1)):
+        for halo, halo8, m16 in ((0, 1, 0), (1, 0, 0), (1, 1, 0), (2, 1, 0), (1, 0, 1), (1, 1, 1), (2, 1, 1)):
             call("avt_set_halo", halo)
             call("avt_set_halo8", halo8)
+            call("avt_set_halo_mf16", m16)
             y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
             acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
             call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
@@ -271,6 +280,7 @@ def test_halo_matches_gather(case):
     finally:
         call("avt_set_halo", 1)
         call("avt_set_halo8", -1)
+        call("avt_set_halo_mf16", -1)
     (y0, dx0, a0) = outs[0]
     # 4-wave 128x128 and 8-wave 256x128 halo forms for W <= 19 (avt_set_halo8), the 8-wave forms for W <= 79
     for y1, dx1, a1 in outs[1:]:
@@ -423,7 +433,7 @@ def test_stem_fwd_wgrad(cin, cp, H, W, N):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_dgrad(case, tiles):
+def test_conv_dgrad(case, tiles, mf16):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     dy = _rand_act(N, Pq, Qq, K, 5)
@@ -957,7 +967,7 @@ def _bn_stats_rand(C, seed):
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("mode", ["relu_fma", "mask_y", "two_bn"])
-def test_conv_dgrad_bn_epilogue(case, mode):
+def test_conv_dgrad_bn_epilogue(case, mode, mf16):
     """avt_conv2d_dgrad_bn: the store epilogue masks the dgrad result by the BN's ReLU (recomputed from
     (xc, scale, shift) or read from y) and accumulates that BN's backward reductions (and a second
     BN's) -- bitwise the masked plain-dgrad result, sums == fp64 sums of it; then

@@ -70,7 +70,8 @@ def test_splitk_fwd(case, ks):
     for _ in range(2):
         y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
         acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
-        call("avt_conv2d_fwd_ws", P(xd), P(wf), P(y), P(acc), N, H, W, C, K, 3, 3, 1, 1, kg, P(part), P(cnt), S())
+        call("avt_conv2d_fwd_ws", P(xd), P(wf), P(y), P(acc), N, H, W, C, K, 3, 3, 1, 1, kg, P(part), part.numel(),
+             P(cnt), cnt.numel(), S())
         torch.cuda.synchronize()
         outs.append((y, acc))
     assert cnt.abs().max().item() == 0  # tickets left zero for the next launch
@@ -114,7 +115,7 @@ def test_splitk_dgrad(case, ks, mode):
     for _ in range(2):
         dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
         call("avt_conv2d_dgrad_ws", P(dyd), P(wt), P(dx), P(addd), P(bitsd), N, H, W, C, K, 3, 3, 1, 1, P(part),
-             P(cnt), S())
+             part.numel(), P(cnt), cnt.numel(), S())
         torch.cuda.synchronize()
         outs.append(dx)
     assert cnt.abs().max().item() == 0
@@ -129,3 +130,30 @@ def test_splitk_dgrad(case, ks, mode):
             a = a * m
         ref = ref + a
     assert rel_err(outs[0], ref) < 8e-3
+
+
+def test_splitk_workspace_too_small_runs_unsplit():
+    """A workspace sized for one plan, called after the knobs changed to a larger one: the call
+    re-plans, sees the plan does not fit and runs without split-K -- bitwise equal to avt_conv2d_fwd."""
+    N, H, W, C, K = 2, 17, 19, 512, 512
+    call("avt_set_halo_splitk", 2, 0)
+    nf, nc = _plan(N, H, W, C, K, False)
+    assert nc > 0
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, H, W, C, generator=g).relu().to(torch.bfloat16).to(DEV)
+    w = (torch.randn(K, 3, 3, C, generator=g) * (2.0 / (K * 9)) ** 0.5).float()
+    kg = 9 * C
+    wf = torch.empty(K, kg, device=DEV, dtype=torch.bfloat16)
+    call("avt_pack_conv_weight", P(w.to(DEV)), K, 3, 3, C, C, kg, P(wf), None, S())
+    part = torch.empty(nf, device=DEV)
+    cnt = torch.zeros(nc, device=DEV, dtype=torch.int32)
+    call("avt_set_halo_splitk", 8, 0)  # needs 4x the partials the workspace holds
+    y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+    call("avt_conv2d_fwd_ws", P(x), P(wf), P(y), None, N, H, W, C, K, 3, 3, 1, 1, kg, P(part), part.numel(), P(cnt),
+         cnt.numel(), S())
+    call("avt_set_halo_splitk", 1, 0)
+    y0 = torch.empty_like(y)
+    call("avt_conv2d_fwd", P(x), P(wf), P(y0), None, N, H, W, C, K, 3, 3, 1, 1, kg, S())
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    assert cnt.abs().max().item() == 0

@@ -29,8 +29,8 @@ def load(d, ctr):
     return tot, cnt
 
 
-def main():
-    d, steps = sys.argv[1], float(sys.argv[2])
+def kernel_rows(d):
+    """[(kernel, dispatches, read bytes, write bytes)] over the whole run, largest first."""
     fetch, nf = load(d, "FETCH_SIZE")
     write, _ = load(d, "WRITE_SIZE")
     rows = []
@@ -39,6 +39,29 @@ def main():
         wr = write.get(k, 0.0) * 1024.0
         rows.append((k, nf.get(k, 0), rd, wr))
     rows.sort(key=lambda r: -(r[2] + r[3]))
+    return rows
+
+
+def summarize(d, steps, batch, source, lib_hash=None):
+    """The per-step traffic record bench.py reads (conv family, BN family, whole step, per kernel)."""
+    rows = kernel_rows(d)
+    conv = [r for r in rows if any(c in r[0] for c in CONV)]
+    conv_rd, conv_wr, conv_n = sum(r[2] for r in conv), sum(r[3] for r in conv), sum(r[1] for r in conv)
+    bn_b = sum(rd + wr for k, n, rd, wr in rows if any(c in k for c in BN))
+    tot_b = sum(rd + wr for k, n, rd, wr in rows)
+    return {"per_gpu_batch": batch, "source": source, "lib_source_hash": lib_hash,
+            "conv_dispatches_per_step": conv_n / steps, "conv_read_bytes_per_step": conv_rd / steps,
+            "conv_write_bytes_per_step": conv_wr / steps,
+            "conv_bytes_per_dispatch": (conv_rd + conv_wr) / max(conv_n, 1),
+            "conv_kernels": sorted({r[0][:120] for r in conv}),
+            "step_bytes": tot_b / steps, "bn_family_bytes_per_step": bn_b / steps,
+            "per_kernel": {k[:120]: {"dispatches_per_step": n / steps, "read_bytes_per_step": rd / steps,
+                                     "write_bytes_per_step": wr / steps} for k, n, rd, wr in rows}}
+
+
+def main():
+    d, steps = sys.argv[1], float(sys.argv[2])
+    rows = kernel_rows(d)
     conv_rd = conv_wr = 0.0
     conv_n = 0
     for k, n, rd, wr in rows:
@@ -61,14 +84,9 @@ def main():
     if "--json" in sys.argv:
         out = sys.argv[sys.argv.index("--json") + 1]
         batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 128
-        json.dump({"per_gpu_batch": batch, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py "
-                   "--no-graph (tools/pmc_traffic.sh); read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB",
-                   "conv_dispatches_per_step": conv_n / steps, "conv_read_bytes_per_step": conv_rd / steps,
-                   "conv_write_bytes_per_step": conv_wr / steps,
-                   "conv_bytes_per_dispatch": (conv_rd + conv_wr) / max(conv_n, 1),
-                   "step_bytes": tot_b / steps, "bn_family_bytes_per_step": bn_b / steps,
-                   "per_kernel": {k[:120]: {"dispatches_per_step": n / steps, "read_bytes_per_step": rd / steps,
-                                            "write_bytes_per_step": wr / steps} for k, n, rd, wr in rows}},
+        lib_hash = sys.argv[sys.argv.index("--lib-hash") + 1] if "--lib-hash" in sys.argv else None
+        json.dump(summarize(d, steps, batch, "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --no-graph "
+                            "(tools/pmc_traffic.sh); read = 2 x FETCH_SIZE KiB, write = WRITE_SIZE KiB", lib_hash),
                   open(out, "w"), indent=1)
 
 
