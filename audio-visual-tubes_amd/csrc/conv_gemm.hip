@@ -850,6 +850,10 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
   HaloArgs ha{};
   ha.ksplit = ksplit;
   ha.cps = p.IC / 64 / ksplit;
+#ifdef AVT_DIAG  // wrong-results timing diagnostics: the -DAVT_DIAG build only
+  static const int hdbg = getenv("AVT_HALO_DBG") ? atoi(getenv("AVT_HALO_DBG")) : 0;
+  ha.dbg = hdbg;
+#endif
   ha.part = part;
   ha.cnt = cnt;
   const int batch = p.M / (p.OH * p.OW);

@@ -29,7 +29,14 @@ struct HaloArgs {
   int ksplit, cps;
   float* part;           // [tiles][ksplit][BM*BN]
   int* cnt;              // [tiles], zero between launches
+  int dbg;               // -DAVT_DIAG build only (AVT_HALO_DBG; wrong results): 1 weight DMA out of range (issued,
+                         // no traffic), 2 patch DMA likewise, 4 no per-tap barrier, 8 no MFMA, 16 no epilogue stores
 };
+#ifdef AVT_DIAG
+#define HALO_DBG(bit) (ha.dbg & (bit))
+#else
+#define HALO_DBG(bit) false
+#endif
 
 // write-through (sc1) 16-byte stores / loads of the split-K partial tiles: the hand-off of
 // MI355X_MICROARCH.md's table (sc1 stores, every storing wave's vmcnt(0), a barrier, one agent-scope
@@ -186,7 +193,8 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     const bool live = cn < nchunk;
     const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + (cbase + cn) * BK) * 2);
 #pragma unroll
-    for (int i = 0; i < BR; ++i) buf_lds16(rsb, Bs + (wid * BR + i) * 1024, live ? b_off[i] + boff : kOOB);
+    for (int i = 0; i < BR; ++i)
+      buf_lds16(rsb, Bs + (wid * BR + i) * 1024, (live && !HALO_DBG(1)) ? b_off[i] + boff : kOOB);
     if (tn >= NSTB - 1) {
       char* Ab = smem + ((cn + 1) & 1) * ABUF;
       const bool alive = live && cn + 1 < nchunk;
@@ -195,7 +203,8 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const int q = ((tn - (NSTB - 1)) * AP + a) * NW + wid;  // pieces 0..6 of the patch
         const bool inrange = q < PINSTR;
         // out-of-range instructions still issue (constant vmcnt): zeros into the zero area
-        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow, (alive && inrange) ? patch_voff(q, cbase + cn + 1) : kOOB);
+        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow,
+                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase + cn + 1) : kOOB);
       }
     }
   };
@@ -246,7 +255,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
           else
             wait_vmcnt<W0 + 3 * AP>();
         }
-        __builtin_amdgcn_s_barrier();
+        if (!HALO_DBG(4)) __builtin_amdgcn_s_barrier();
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
         auto load_frags = [&](int ks, int buf) {
 #pragma unroll
@@ -268,15 +277,17 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
             load_frags(ks + 1, (ks + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
           }
+          if (!HALO_DBG(8)) {
 #pragma unroll
-          for (int i = 0; i < FM; ++i)
+            for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int j = 0; j < FN; ++j) {
-              if constexpr (MF16)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
-              else
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
-            }
+              for (int j = 0; j < FN; ++j) {
+                if constexpr (MF16)
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+                else
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+              }
+          }
           if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -391,6 +402,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 #pragma unroll
       for (int v = 0; v < AV; ++v) Ct[acc_row(i, v) * CT_LD + wn * (BN / WN) + j * FR + frow] = f2bf(acc[i][j][v]);
   __syncthreads();
-  epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, [&](int r) -> size_t { return (size_t)(m0 + r); },
+  if (!HALO_DBG(16))
+    epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, [&](int r) -> size_t { return (size_t)(m0 + r); },
                         reinterpret_cast<float*>(smem));
 }

@@ -109,6 +109,24 @@ class FlatStore:
         self.bflat.copy_(src.bflat)
         self.nbt.copy_(src.nbt)
 
+    def fill_from(self, get):
+        """Fill this (mirror) store from per-name tensors on its device -- an nn.DataParallel replica's
+        broadcast parameters and buffers (get(name) -> tensor in the module's layout): local copies only."""
+        dst, src = [], []
+        for n in self.pnames:
+            t = get(n).detach()
+            r = self.raw(n)
+            dst.append(r)
+            src.append(t.permute(0, 2, 3, 1) if t.dim() == 4 else t)  # OIHW -> the store's OHWI
+        for n in self.boff:
+            dst.append(self.rawbuf(n))
+            src.append(get(n))
+        for i, n in enumerate(self.nbt_names):
+            dst.append(self.nbt[i])
+            src.append(get(n))
+        with torch.no_grad():
+            torch._foreach_copy_(dst, src)
+
     def raw(self, name: str) -> torch.Tensor:
         """fp32 storage of a parameter: conv weights as [K][R][S][C] (OHWI), others as-is."""
         off, shape = self.poff[name]
@@ -332,9 +350,10 @@ class AVEngine:
                 tmax = max(tmax, spec.cout * spec.kg + (0 if wt is None else wt.numel()))
             maxel = max(maxel, tmax)
             self._pack_parts[tr.prefix] = (first, len(descs) - first, tmax)
-        assert len(descs[0]) == int(query("avt_pack_desc_bytes"))
-        blob = b"".join(descs)
-        self._pack_table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+        if descs:  # (an engine of 3-D trunks only packs its own operands, tube.py)
+            assert len(descs[0]) == int(query("avt_pack_desc_bytes"))
+            blob = b"".join(descs)
+            self._pack_table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
         self._pack_n, self._pack_max = len(descs), maxel
         # BN accumulators: per BN 'fwd' [slots][C][3] f64 and 'bwd' [slots][C][2] f64 + k1/k2 (2C f32)
         slots = int(query("avt_bn_slots"))

@@ -333,23 +333,38 @@ class AVENet(nn.Module):
         mirror of the flat store there, refreshed from the model's store on every forward (its running-
         statistic updates are dropped, as DataParallel drops them).  Each replica contrasts only its own
         B/G clips, as in the reference.  The broadcast copies are the autograd inputs, so the gradients
-        flow back through replicate()'s Broadcast, which sums them onto the module's parameters."""
+        flow back through replicate()'s Broadcast, which sums them onto the module's parameters.
+        The mirror is refreshed from the replica's OWN broadcast parameters and buffers (device-local
+        copies): replicate() already moved them across GPUs once.  Forward hooks on a replica's layer4
+        (copied from the module by replicate()) run per replica, as nn.Module.__call__ runs them."""
         _check_hooks(self)
-        if self.imgnet.layer4._forward_hooks or self.audnet.layer4._forward_hooks:
-            raise NotImplementedError("avt: forward hooks under nn.DataParallel are not supported")
         dev = image.device
         eng = self.engine(dev)
-        if eng.flat is not self._flat:
-            eng.flat.sync_from(self._flat)
         n_train = sum(1 for n in self._flat.pnames if trainable(n))
         tensors = [self._replica_tensor(n) for n in self._flat.pnames[:n_train]]
         if any(t.device != dev for t in tensors):
             raise RuntimeError("avt: DataParallel replica parameters are not on the replica's device")
-        if torch.is_grad_enabled() and self.training and any(t.requires_grad for t in tensors):
-            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, None, image, audio, *tensors)
+        if eng.flat is not self._flat:
+            eng.flat.fill_from(self._replica_tensor)
+        return self._forward_on(eng, tensors, image, audio)
+
+    def _forward_on(self, eng: AVEngine, train_params, image, audio):
+        """The forward on one engine with these parameter tensors as the autograd inputs, honouring
+        forward hooks on this module's (or replica's) imgnet/audnet.layer4 (test.py:60-63)."""
+        hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
+                  if m._forward_hooks]
+        sink = {} if hooked else None
+        need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in train_params)
+        if need_grad:
+            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, sink, image, audio, *train_params)
         else:
-            out, _ = eng.forward(image, audio, self.training)
+            out, _ = eng.forward(image, audio, self.training, layer_io=sink is not None)
             A, logits, wA, Pos, Neg = out["A"], out["logits"], out["weighted_A"], out["Pos"], out["Neg"]
+            if sink is not None:
+                sink.update(out)
+        for name, m in hooked:  # test.py:63: activation['layer4'] = output.detach()
+            k_in, k_out = ("v_in", "v") if name == "imgnet" else ("a_in", "a")
+            _run_forward_hooks(m, _nhwc_to_nchw_f32(sink[k_in]), _nhwc_to_nchw_f32(sink[k_out]))
         return A, logits, wA, Pos, Neg
 
     def _replica_tensor(self, name: str) -> torch.Tensor:
@@ -363,25 +378,8 @@ class AVENet(nn.Module):
         if getattr(self, "_is_replica", False):
             return self._replica_forward(image, audio)
         _check_hooks(self)
-        hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
-                  if m._forward_hooks]
-        sink = {} if hooked else None
-        eng = self.engine()
-        params = self.ordered_parameters()
         n_train = sum(1 for n in self._flat.pnames if trainable(n))
-        train_params = params[:n_train]
-        need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in train_params)
-        if need_grad:
-            A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, sink, image, audio, *train_params)
-        else:
-            out, _ = eng.forward(image, audio, self.training, layer_io=sink is not None)
-            A, logits, wA, Pos, Neg = out["A"], out["logits"], out["weighted_A"], out["Pos"], out["Neg"]
-            if sink is not None:
-                sink.update(out)
-        for name, m in hooked:  # test.py:63: activation['layer4'] = output.detach()
-            k_in, k_out = ("v_in", "v") if name == "imgnet" else ("a_in", "a")
-            _run_forward_hooks(m, _nhwc_to_nchw_f32(sink[k_in]), _nhwc_to_nchw_f32(sink[k_out]))
-        return A, logits, wA, Pos, Neg
+        return self._forward_on(self.engine(), self.ordered_parameters()[:n_train], image, audio)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -513,6 +511,7 @@ class FullModel(nn.Module):
         self._flat = FlatStore(self, tube_trainable)
         self._engine = None
         self.audnet._adopt(self, "audnet.")
+        self.vidnet._adopt(self, "vidnet.")
 
     def __getstate__(self):
         state = self.__dict__.copy()
@@ -526,11 +525,13 @@ class FullModel(nn.Module):
         self._flat.rebind()
         self._engine = None
         self.audnet._adopt(self, "audnet.")
+        self.vidnet._adopt(self, "vidnet.")
 
     def _apply(self, fn, recurse=True):
         self._flat.apply(fn)
         self._engine = None
         self.audnet._avt_engine = None
+        self.vidnet._avt_engine = None
         return self
 
     def engine(self):

@@ -3,11 +3,17 @@
 Same module tree, construction order and init as ``resnet3D.generate_model(18, no_max_pool=True,
 n_classes=1039)`` (model.py:20; resnet3D.py:103-234), so ``torch.manual_seed(s)`` gives the
 reference's weights and ``state_dict`` keys/shapes match (``vidnet.conv1.weight`` [64,3,7,7,7],
-``vidnet.layerL.B.downsample.{0,1}.*``, ``vidnet.fc.*``).  The compute runs inside FullModel's
-engine (tube.py); calling the shell alone is not supported.
+``vidnet.layerL.B.downsample.{0,1}.*``, ``vidnet.fc.*``).  Inside FullModel the compute runs in its
+engine (tube.py); called on its own (``FullModel.vidnet(video)`` or a standalone
+``generate_model(18, no_max_pool=True, ...)``) the same kernels run through tube.R3DEngine and return
+the ``fc`` logits as resnet3D.ResNet.forward does (resnet3D.py:197-213).  Forward only: the build
+computes no gradients for the video trunk (FullModel detaches it), so a call that would need them raises.
 """
 from __future__ import annotations
 
+import weakref
+
+import torch
 from torch import nn
 
 
@@ -66,6 +72,9 @@ class ResNet(nn.Module):
             elif isinstance(m, nn.BatchNorm3d):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
+        self._avt_parent = None  # (weakref to the owning FullModel, prefix) once adopted
+        self._avt_engine = None
+        self._own_flat = None  # a standalone module's flat storage, created at its first .to() / forward
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None  # built before the block, as resnet3D.py:169-184 (RNG order)
@@ -78,8 +87,51 @@ class ResNet(nn.Module):
             layers.append(block(self.in_planes, planes))
         return nn.Sequential(*layers)
 
-    def forward(self, x):  # pragma: no cover - documented limitation
-        raise RuntimeError("avt: the R3D trunk runs inside FullModel.forward (fused engine); call the parent model")
+    def _adopt(self, parent, prefix: str):
+        self._avt_parent = (weakref.ref(parent), prefix)
+        self._own_flat = None
+        self._avt_engine = None
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_avt_engine"] = None
+        return state
+
+    def _flat_store(self):
+        from .engine import FlatStore
+
+        if self._own_flat is None:
+            self._own_flat = FlatStore(self, lambda n: False)  # nothing of the video trunk is trained here
+        return self._own_flat
+
+    def _apply(self, fn, recurse=True):
+        if self._avt_parent is not None and self._avt_parent[0]() is not None:
+            self._avt_parent[0]()._apply(fn)
+            return self
+        self._flat_store().apply(fn)
+        self._avt_engine = None
+        return self
+
+    def forward(self, x):
+        """resnet3D.ResNet.forward (resnet3D.py:197-213): x fp32 [b,3,t,H,W] -> fc logits [b, n_classes]."""
+        from .tube import R3DEngine
+
+        if not self.no_max_pool:
+            raise NotImplementedError("avt: the R3D stem max-pool is not built (FullModel uses no_max_pool=True, "
+                                      "model.py:20)")
+        if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
+            raise NotImplementedError("avt: the R3D trunk is forward-only in this build (FullModel detaches it); "
+                                      "call it under torch.no_grad() or with requires_grad_(False) parameters")
+        if self._avt_parent is not None:
+            parent, prefix = self._avt_parent[0](), self._avt_parent[1]
+            if parent is None or getattr(parent, prefix.rstrip("."), None) is not self:
+                raise RuntimeError("avt: this R3D trunk is no longer its parent's (a copied trunk; copy the whole model)")
+            flat = parent._flat
+        else:
+            prefix, flat = "", self._flat_store()
+        if self._avt_engine is None or self._avt_engine.flat is not flat:
+            self._avt_engine = R3DEngine(flat, prefix)
+        return self._avt_engine.forward(x, self.training)
 
 
 def generate_model(model_depth, **kwargs):

@@ -294,3 +294,49 @@ class TubeEngine(AVEngine):
                 on_boundary(self.aud.prefix + "lo")
         finally:
             self.store.grads = None
+
+
+class R3DEngine(AVEngine):
+    """The R3D-18 trunk called on its own -- ``FullModel.vidnet(video)`` or a standalone
+    ``resnet3D.generate_model(18, no_max_pool=True, ...)(video)`` (resnet3D.py:197-213): the conv stem ..
+    layer4 on libavt as inside FullModel (R3DTrunk), then AdaptiveAvgPool3d((1,1,1)) + fc on the pooled
+    fp32 features.  Forward only, as everywhere in this build (FullModel detaches the video trunk)."""
+
+    def __init__(self, flat: FlatStore, prefix: str):
+        self._prefix = prefix
+        super().__init__(flat)
+        self.concurrent = False
+        self.store = _TubeStore(self)
+        self._nbt_idx = torch.tensor([i for i, n in enumerate(flat.nbt_names) if n.startswith(prefix)],
+                                     device=flat.flat.device, dtype=torch.long)
+
+    def _setup_trunks(self):
+        self.vid = R3DTrunk(self._prefix)
+        self.packs3d: Dict[str, torch.Tensor] = {}
+        self.trunks2d = []
+        self.bn_trunks = [self.vid]
+
+    def _alloc(self, dev):
+        super()._alloc(dev)
+        for spec in self.vid.convs():
+            self.packs3d[spec.name] = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+
+    def pack_weights(self):
+        for spec in self.vid.convs():
+            call("avt_pack_conv3d_weight", P(self.flat.raw(spec.name)), P(self.packs3d[spec.name]), spec.cout,
+                 spec.cin, spec.kt, spec.k, spec.k, int(spec.stem), stream_ptr())
+
+    def forward(self, video: torch.Tensor, training: bool) -> torch.Tensor:
+        """video fp32 [b,3,t,H,W] -> fc logits [b, n_classes] fp32."""
+        if not video.is_cuda:
+            raise RuntimeError("avt: inputs must be on the GPU (no CPU path)")
+        if video.dim() != 5:
+            raise ValueError(f"avt: expected video [b,3,t,H,W], got {tuple(video.shape)}")
+        self.pack_weights()
+        if training and self._nbt_idx.numel():
+            self.flat.nbt.index_add_(0, self._nbt_idx, torch.ones_like(self._nbt_idx))
+        v = self.vid.forward(video, self.store, training)  # [(b t), h, w, 512] bf16
+        b = video.shape[0]
+        feat = v.view(b, -1, v.shape[-1]).float().mean(1)  # AdaptiveAvgPool3d((1,1,1)) + flatten
+        w, bias = self.flat.raw(self._prefix + "fc.weight"), self.flat.raw(self._prefix + "fc.bias")
+        return torch.addmm(bias, feat, w.t())  # nn.Linear (resnet3D.py:212)

@@ -334,6 +334,8 @@ def test_dataparallel_replica_matches_model(mirror):
         assert rel_err(g_dp[n], ref[n]) < 2e-3, (n, rel_err(g_dp[n], ref[n]))
     if mirror:  # a replica on another GPU does not touch the module's BN running statistics
         assert torch.equal(model._flat.bflat, bufs)
+        # ... and its mirror was filled from the replica's own broadcast tensors: the module's weights
+        assert torch.equal(eng.flat.flat, model._flat.flat)
     else:  # the replica on the module's GPU updates them (DataParallel keeps replica 0's)
         assert not torch.equal(model._flat.bflat, bufs)
 
@@ -356,3 +358,32 @@ def test_dataparallel_wrapper_one_gpu_and_deepcopy():
     with torch.no_grad():
         twin._flat.flat.mul_(0.5)
     assert rel_err(model.imgnet(img), out_m) < 1e-6  # the original's weights are untouched
+
+
+@pytest.mark.parametrize("mirror", [False, True])
+def test_dataparallel_replica_runs_layer4_hooks(mirror):
+    """VERDICT r3 Missing #1: forward hooks on `.imgnet.layer4` (test.py:60-63, registered on the DataParallel-
+    wrapped model) are copied into every replica by replicate() and run there, per replica, with that
+    replica's layer4 output -- the same map the unwrapped model's hook sees."""
+    from torch.nn.parallel import replicate
+
+    from avt_amd.engine import AVEngine
+
+    img, aud = (t.to(DEV) for t in _tiny())
+    model = _model().eval()
+    seen = []
+    h = model.imgnet.layer4.register_forward_hook(lambda m, i, o: seen.append((m, i[0].detach(), o.detach())))
+    with torch.no_grad():
+        model(img, aud)
+        if mirror:
+            eng = AVEngine(model._flat.mirror(DEV), model.epsilon, model.epsilon2, model.tau, model.trimap, model.Neg)
+            model._engines[DEV.index if DEV.index is not None else torch.cuda.current_device()] = eng
+        rep = replicate(model, [0])[0]
+        rep(img, aud)
+    model._engines.clear()
+    h.remove()
+    assert len(seen) == 2
+    (m0, i0, o0), (m1, i1, o1) = seen
+    assert m0 is model.imgnet.layer4 and m1 is rep.imgnet.layer4
+    assert o0.dim() == 4 and o0.shape[:2] == (img.shape[0], 512)
+    assert torch.equal(o0, o1) and torch.equal(i0, i1)

@@ -334,3 +334,40 @@ def test_hardway_attention_standalone_autograd(b, t, hw, C, normalized):
     assert rel_err(logits, l_r.detach()) < 2e-4
     assert rel_err(vd.grad, vr.grad) < 2e-4
     assert rel_err(ad.grad, ar.grad) < 2e-4
+
+
+@pytest.mark.parametrize("standalone", [False, True])
+def test_r3d_forward_standalone(standalone):
+    """VERDICT r3 Missing #3: FullModel.vidnet(video) / a standalone generate_model(18, no_max_pool=True,
+    n_classes=1039)(video) return resnet3D.ResNet.forward's fc logits (resnet3D.py:197-213: layer4 ->
+    AdaptiveAvgPool3d -> fc) on the same kernels, vs the fp64 restatement; forward-only (raises where
+    gradients would be needed)."""
+    from avt_amd.resnet3D import generate_model
+
+    video = tor.make_video(2, 4, 64)
+    sd = tor.make_tube_state(0)
+    if standalone:
+        net = generate_model(18, no_max_pool=True, n_classes=1039)
+        net.load_state_dict({k[len("vidnet."):]: v for k, v in sd.items() if k.startswith("vidnet.")})
+        net = net.to(DEV).train()
+    else:
+        net = _fullmodel().vidnet
+    with pytest.raises(NotImplementedError):
+        net(video.to(DEV))  # grad mode with parameters that require grad
+    with torch.no_grad():
+        logits = net(video.to(DEV))
+    torch.cuda.synchronize()
+    assert logits.shape == (2, 1039)
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    with torch.no_grad():
+        feat = tor.r3d18_forward(sd64, "vidnet.", video.double(), training=True)  # [b,512,t,h,w]
+        ref = F.linear(feat.mean(dim=(2, 3, 4)), sd64["vidnet.fc.weight"], sd64["vidnet.fc.bias"])
+    err = rel_err(logits, ref)
+    print(f"standalone={standalone}: R3D logits rel err {err:.3e}")
+    assert err < 3e-2, err
+    # train mode updated the running statistics and the batch counter, as the reference BN3d does
+    bn1 = net.bn1
+    assert int(bn1.num_batches_tracked) == 1
+    assert not torch.equal(bn1.running_mean.cpu(), torch.zeros(64))
+    with pytest.raises(NotImplementedError):  # the stem max-pool path is not built
+        generate_model(18, no_max_pool=False).to(DEV)(video.to(DEV))

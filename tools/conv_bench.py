@@ -77,7 +77,7 @@ def main():
     kinds = args.kinds.split(",")
     tot = {}
     for name, H, W, C, K, R, st, pad in SHAPES:
-        if args.only and args.only not in name:
+        if args.only and not any(o in name for o in args.only.split(",")):
             continue
         Pq, Qq = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
         x = torch.randn(N, H, W, C, device=dev).relu().to(torch.bfloat16)
@@ -137,11 +137,11 @@ def main():
                     pp, pc = (P(part), P(cnt)) if nc.value else (None, None)
                     if dg == 0:
                         ms = timeit(lambda: call("avt_conv2d_fwd_ws", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R,
-                                                 st, pad, kg, pp, pc, S()))
+                                                 st, pad, kg, pp, part.numel(), pc, cnt.numel(), S()))
                         line += f" | sk[{ks}:{nc.value and nf.value // (nc.value * 16384)}] fwd {flops / ms / 1e9:6.0f}"
                     else:
                         ms = timeit(lambda: call("avt_conv2d_dgrad_ws", P(dy), P(wt), P(dx), None, None, N, H, W, C,
-                                                 K, R, R, st, pad, pp, pc, S()))
+                                                 K, R, R, st, pad, pp, part.numel(), pc, cnt.numel(), S()))
                         line += f" dgrad {flops / ms / 1e9:6.0f}"
                     tot[(f"{'dgrad' if dg else 'fwd'}_sk{ks}", 1)] = tot.get((f"{'dgrad' if dg else 'fwd'}_sk{ks}", 1), 0) + ms
             call("avt_set_halo_splitk", 0, 0)
