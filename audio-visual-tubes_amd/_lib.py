@@ -28,7 +28,7 @@ class DgradBnEpi(ctypes.Structure):
     """avt_dgrad_bn_epi (include/avt.h): the BatchNorm-backward epilogue of avt_conv2d_dgrad_bn."""
     _fields_ = [("xc", ctypes.c_void_p), ("y", ctypes.c_void_p), ("stats", ctypes.c_void_p),
                 ("acc", ctypes.c_void_p), ("xc2", ctypes.c_void_p), ("stats2", ctypes.c_void_p),
-                ("acc2", ctypes.c_void_p), ("skip_class00", ctypes.c_int)]
+                ("acc2", ctypes.c_void_p), ("skip_class00", ctypes.c_int), ("append_slots", ctypes.c_int)]
 
 
 class BnBwdTarget(ctypes.Structure):
@@ -36,12 +36,6 @@ class BnBwdTarget(ctypes.Structure):
     _fields_ = [("xc", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
                 ("gamma", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
                 ("gc", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
-
-
-class BnStat(ctypes.Structure):
-    """avt_bn_stat (include/avt.h): one train-mode BatchNorm's statistics for avt_bn_apply_fin."""
-    _fields_ = [("acc", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
-                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
 
 
 # name -> (restype, argtypes)
@@ -52,7 +46,6 @@ SIGNATURES = {
     "avt_peak_mfma": (_I, [_P, _I, _I, _I, ctypes.c_uint, _P]),
     "avt_peak_mfma_flops": (_L, [_I, _I, _I]),
     "avt_copy16": (_I, [_P, _P, _Z, _I, _P]),
-    "avt_bn_slots": (_I, []),
     "avt_set_conv_variant": (_I, [_I]),
     "avt_set_wgrad_policy": (_I, [_I, _I]),
     "avt_set_nt64_config": (_I, [_I]),
@@ -69,7 +62,7 @@ SIGNATURES = {
     "avt_set_wgrad_tiles": (_I, [_I]),
     "avt_set_small_tiles": (_I, [_I]),
     "avt_set_wgrad_halo": (_I, [_I]),
-    "avt_bn_acc_doubles": (_Z, [_I]),
+    "avt_bn_acc_doubles": (_Z, [_L, _I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad_bn": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(DgradBnEpi), _P]),
@@ -81,8 +74,6 @@ SIGNATURES = {
     "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
     "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),
-    "avt_bn_apply_fin": (_I, [_P, ctypes.POINTER(BnStat), _P, ctypes.POINTER(BnStat), _P, _P, _L, _L, _I, _I, _F, _F,
-                              _P]),
     "avt_bn_bwd_mask": (_I, [_P, _P, ctypes.POINTER(BnBwdTarget), ctypes.POINTER(BnBwdTarget), _L, _I, _P]),
     "avt_conv2d_wgrad_workspace": (_Z, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P]),
@@ -109,9 +100,10 @@ SIGNATURES = {
     "avt_hardway_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I,
                              _P]),
     "avt_hardway_bwd_ex": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                _P, _P, _I, _P]),
+                                _P, _P, _I, _P, _P]),
+    "avt_hardway_bwd_ws_floats": (_Z, [_I, _I]),
     "avt_hardway_attention_fwd": (_I, [_P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "avt_hardway_attention_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P]),
+    "avt_hardway_attention_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P]),
     "avt_twoview_loss": (_I, [_P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "avt_loss_workspace_floats": (_Z, [_L, _L]),
     "avt_propagation_loss": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),

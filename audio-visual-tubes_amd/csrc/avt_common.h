@@ -18,13 +18,37 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define AVT_OK 0
 #define AVT_EINVAL -1
 #define AVT_EHIP -2
-// spread of the fp64 BN statistic accumulators (atomic contention); a multiple of 16.  64 measured -1 %
-// at B=32 and B=128 against 16 (tools/build_variant.sh libavt_base.so -DAVT_BN_SLOTS=..., tools/r3_slots.sh)
-#ifndef AVT_BN_SLOTS
-#define AVT_BN_SLOTS 16
-#endif
 
 namespace avt {
+
+// ---- BatchNorm statistic accumulators (deterministic; include/avt.h "BatchNorm statistics") ----
+// fp64 [kBnHdr header][bwd only: k1, k2 = 2C floats = C doubles][slot][C][W] (W = 3 fwd: sum, M2, sum^2/n;
+// W = 2 bwd: sum g', sum g'*xhat).  Every slot is written by exactly ONE block of the accumulating launch, with
+// plain stores (no atomics, no zeroing); header[0] = the slots that launch wrote, header[1] = slots a second
+// launch appended after them (a stride-2 dgrad's downsample twin, conv_epi.h).  The finalize kernels sum
+// the slots in slot order, so the statistics -- and everything downstream -- are the same bits on every
+// run.  Capacity: one slot per 64 rows (the smallest row tile) + 520 (persistent / reduce grids <= 512).
+constexpr int kBnHdr = 8;
+__host__ __device__ inline long long bn_slot_cap(long long rows) { return (rows + 63) / 64 + 520; }
+__device__ __forceinline__ double* bn_fwd_slots(double* acc) { return acc + kBnHdr; }
+__device__ __forceinline__ double* bn_bwd_slots(double* acc, int C) { return acc + kBnHdr + C; }
+// the launch's slot count, recorded by ONE block of it (`leader`: a block that surely reaches the call);
+// append: after the slots of the launch it appends to -- header[0], written by that earlier launch on the same
+// stream (bn_slot_base) -- into header[1]
+__device__ __forceinline__ void bn_write_header(double* acc, int nslots, int append, bool leader) {
+  if (leader && threadIdx.x == 0) {
+    if (append) {
+      acc[1] = (double)nslots;
+    } else {
+      acc[0] = (double)nslots;
+      acc[1] = 0.0;
+    }
+  }
+}
+__device__ __forceinline__ void bn_write_header(double* acc, int nslots, int append) {
+  bn_write_header(acc, nslots, append, blockIdx.x == 0);
+}
+__device__ __forceinline__ int bn_slot_base(const double* acc, int append) { return append ? (int)acc[0] : 0; }
 
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);

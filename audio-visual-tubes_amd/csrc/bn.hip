@@ -3,13 +3,14 @@
 // models/base_models.py:39,46-49,120-121,141 (eps 1e-5, momentum 0.1): normalise with the biased
 // batch variance, update running_var with the unbiased one.
 //
-//   fwd : the conv epilogue adds per-128-row-tile (sum_t, M2_t, sum_t^2/n_t) into an fp64
-//         accumulator [AVT_BN_SLOTS][C][3]; bn_finalize merges the slots exactly
-//         (M2 = sum M2_t + sum sum_t^2/n_t - S^2/N, Chan's formula), writes scale/shift/mean/invstd,
-//         updates running stats and re-zeroes the accumulator; bn_apply (+residual, +ReLU).
-//   bwd : bn_bwd_reduce adds per-block (sum g', sum g'*xhat) (g' = g*[y>0]) into an fp64
-//         accumulator [AVT_BN_SLOTS][C][2] -> bn_bwd_finalize (dgamma, dbeta, k1, k2; re-zeroes) ->
-//         bn_bwd_apply: g_c = gamma*invstd*(g' - k1 - xhat*k2).
+//   fwd : the conv epilogue stores per-row-tile (sum_t, M2_t, sum_t^2/n_t) into its own slot of an fp64
+//         accumulator (avt_common.h: one slot per tile or persistent block, plain stores); bn_finalize
+//         merges the slots in slot order (M2 = sum M2_t + sum sum_t^2/n_t - S^2/N, Chan's formula), writes
+//         scale/shift/mean/invstd and updates the running stats; bn_apply (+residual, +ReLU).
+//   bwd : bn_bwd_reduce stores per-block (sum g', sum g'*xhat) (g' = g*[y>0]) into slot blockIdx of an fp64
+//         accumulator -> bn_bwd_finalize (dgamma, dbeta, k1, k2) -> bn_bwd_apply:
+//         g_c = gamma*invstd*(g' - k1 - xhat*k2).
+//   Deterministic: no atomics; the same inputs give the same bits on every run.
 //         avt_bn_relu_bwd recomputes the ReLU mask from (xc, scale, shift) instead of reading y
 //         (BasicBlock.bn1, base_models.py:47-48); the stem's bn1+relu+maxpool is fused both ways
 //         (avt_stem_*, below) so its full-resolution activation is never stored.
@@ -34,32 +35,37 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// 16 lanes per channel, lane s owning slots s, s+16, s+32, ... (summed in that order): the slot reads
-// (just written by memory-side atomics, so served from memory) are AVT_BN_SLOTS/16 independent loads
-// per lane instead of a dependent chain; the lanes' sums meet by shuffles (fixed tree order).  Launch:
-// 16 channels per 256-thread block.
-static_assert(AVT_BN_SLOTS % 16 == 0, "the finalize kernels spread the slots over 16 lanes");
-constexpr int kSlotsPerLane = AVT_BN_SLOTS / 16;
+// 16 lanes per channel, lane s owning slots s, s+16, s+32, ... in four interleaved partial sums (slots
+// s + 16(4i+q) into partial q, then (p0+p1)+(p2+p3)): independent loads in flight, a fixed summation
+// order; the lanes' sums meet by shuffles in a fixed tree.  Launch: 16 channels per 256-thread block.
 __device__ __forceinline__ double sum16(double v) {
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
   return v;
 }
-// lane s's share of element j of an accumulator [slots][C][W] at channel c (slot stride C*W doubles)
+// lane s's shares of the W elements of channel c over the slots of accumulator acc (header + slots)
 template <int W>
-__device__ __forceinline__ double lane_slots(const double* __restrict__ acc, int C, int c, int s, int j) {
-  const double* p = acc + ((size_t)s * C + c) * W + j;
-  double v = p[0];
+__device__ __forceinline__ void lane_slots(const double* __restrict__ acc, const double* __restrict__ slots, int C,
+                                           int c, int s, double* out) {
+  const int n = (int)acc[0] + (int)acc[1];
+  double p[4][W];
 #pragma unroll
-  for (int k = 1; k < kSlotsPerLane; ++k) v += p[(size_t)k * 16 * C * W];
-  return v;
-}
-template <int W>
-__device__ __forceinline__ void lane_slots_zero(double* __restrict__ acc, int C, int c, int s) {
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-  for (int k = 0; k < kSlotsPerLane; ++k)
+    for (int j = 0; j < W; ++j) p[q][j] = 0.0;
+  int k = s;
+  for (; k + 48 < n; k += 64)
 #pragma unroll
-    for (int j = 0; j < W; ++j) acc[((size_t)(s + 16 * k) * C + c) * W + j] = 0.0;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < W; ++j) p[q][j] += slots[((size_t)(k + 16 * q) * C + c) * W + j];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)  // the tail: at most three slots left (k + 48 >= n)
+    if (k + 16 * q < n)
+#pragma unroll
+      for (int j = 0; j < W; ++j) p[q][j] += slots[((size_t)(k + 16 * q) * C + c) * W + j];
+#pragma unroll
+  for (int j = 0; j < W; ++j) out[j] = (p[0][j] + p[1][j]) + (p[2][j] + p[3][j]);
 }
 
 __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
@@ -70,9 +76,9 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ a
                                                           long long rep) {
   const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
   if (c >= C) return;  // whole 16-lane groups leave together
-  const double S = sum16(lane_slots<3>(acc, C, c, s, 0)), Q = sum16(lane_slots<3>(acc, C, c, s, 1)),
-               R = sum16(lane_slots<3>(acc, C, c, s, 2));
-  lane_slots_zero<3>(acc, C, c, s);
+  double v[3];
+  lane_slots<3>(acc, bn_fwd_slots(acc), C, c, s, v);
+  const double S = sum16(v[0]), Q = sum16(v[1]), R = sum16(v[2]);
   if (s != 0) return;
   const double n = (double)rows;
   const double mean = S / n;
@@ -149,115 +155,6 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
     const u32x4 o = pack8(f);
     reinterpret_cast<u32x4*>(out)[i] = o;
     if (mk) mk[i] = (unsigned char)pos_bits8(o);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// bn_finalize + bn_apply in one launch (avt_bn_apply_fin).  A separate finalize is a dependent launch
-// between the conv and the apply: with the other trunk's long-running conv blocks holding every
-// CU's registers, each such launch waits for a CU (measured: leaving the 40 forward finalize launches
-// out of the graph saves ~1.0 ms of a 10 ms B=128 step and 0.23 ms of the B=32 one).
-// Block b owns channel group g = b % G (64 channels) over pixel chunk b / G: its prologue merges the
-// slots of those 64 channels (4 lanes per channel doing the work of 4 of bn_finalize_kernel's 16, the
-// same fp64 add order -> bitwise the same scale/shift) and the group's first block writes
-// stats [4][C] and the running statistics.  The accumulators are left as they are: the caller zeroes
-// them before the next accumulation (one memset per trunk and forward; a last-block ticket re-zeroing
-// them here serialised ~4096 atomics on one address: +40 us per launch).
-struct BnStatArgs {
-  double* acc;  // [16][C][3] (avt_bn_acc_doubles)
-  const float* gamma;
-  const float* beta;
-  float* rmean;  // null: no running-stat update
-  float* rvar;
-  float* stats;  // [4][C]: scale, shift, mean, invstd
-};
-struct ApplyFinArgs {
-  const bf16_t* x;
-  const bf16_t* res;  // null: no residual
-  bf16_t* out;
-  unsigned char* mk;  // null: no mask bits
-  BnStatArgs bn, bnr;  // bnr.acc null: the residual is added as is
-  long long rows, rep;
-  int C, G, relu, nblk;
-  float momentum, eps;
-};
-
-__device__ __forceinline__ void fin_group(const BnStatArgs& b, int C, int g, long long rows, long long rep,
-                                          float momentum, float eps, bool write, float* sc, float* sh) {
-  const int t = threadIdx.x, cl = t >> 2, q = t & 3, c = g * 64 + cl;
-  double v[4][3];  // the shares of lanes q, q+4, q+8, q+12 of bn_finalize_kernel's 16
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) v[k][j] = lane_slots<3>(b.acc, C, c, q + 4 * k, j);
-  double r[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    // lane q holds slots q, q+4, q+8, q+12: (v_q + v_q+8) + (v_q+4 + v_q+12), then lanes ^2, ^1 -- the
-    // order of sum16's xor 8, 4, 2, 1 tree
-    double s = (v[0][j] + v[2][j]) + (v[1][j] + v[3][j]);
-    s += __shfl_xor(s, 2, 4);
-    s += __shfl_xor(s, 1, 4);
-    r[j] = s;
-  }
-  if (q != 0) return;
-  const double n = (double)rows;
-  const double mean = r[0] / n;
-  double m2 = r[1] + (r[2] - r[0] * mean);
-  if (m2 < 0.0) m2 = 0.0;
-  const float var = (float)(m2 / n);
-  const float inv = rsqrtf(var + eps);
-  const float s_ = b.gamma[c] * inv;
-  const float h_ = b.beta[c] - (float)mean * s_;
-  sc[cl] = s_;
-  sh[cl] = h_;
-  if (!write) return;
-  b.stats[c] = s_;
-  b.stats[C + c] = h_;
-  b.stats[2 * C + c] = (float)mean;
-  b.stats[3 * C + c] = inv;
-  if (b.rmean) {
-    const double nl = n * (double)rep;
-    const float unb = nl > 1.0 ? (float)(m2 * (double)rep / (nl - 1.0)) : var;
-    b.rmean[c] = (1.f - momentum) * b.rmean[c] + momentum * (float)mean;
-    b.rvar[c] = (1.f - momentum) * b.rvar[c] + momentum * unb;
-  }
-}
-
-__global__ __launch_bounds__(256) void bn_apply_fin_kernel(ApplyFinArgs a) {
-  __shared__ float sc[64], sh[64], rsc[64], rsh[64];
-  const int C = a.C, g = blockIdx.x % a.G, pb = blockIdx.x / a.G, npb = a.nblk / a.G;
-  const bool first = pb == 0;
-  fin_group(a.bn, C, g, a.rows, a.rep, a.momentum, a.eps, first, sc, sh);
-  if (a.bnr.acc) fin_group(a.bnr, C, g, a.rows, a.rep, a.momentum, a.eps, first, rsc, rsh);
-  __syncthreads();
-  // 8 lanes per pixel (64 channels), 32 pixels per block pass
-  const int lane8 = threadIdx.x & 7, cl0 = lane8 * 8;
-  const int cv = C / 8;
-  for (long long p = (long long)pb * 32 + (threadIdx.x >> 3); p < a.rows; p += (long long)npb * 32) {
-    const long long i = p * cv + g * 8 + lane8;
-    float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(a.x)[i], f);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = __builtin_fmaf(f[e], sc[cl0 + e], sh[cl0 + e]);
-    if (a.res) {
-      float rr[8];
-      unpack8(reinterpret_cast<const u32x4*>(a.res)[i], rr);
-      if (a.bnr.acc) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += rr[e] * rsc[cl0 + e] + rsh[cl0 + e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] += rr[e];
-      }
-    }
-    if (a.relu) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
-    }
-    const u32x4 o = pack8(f);
-    reinterpret_cast<u32x4*>(a.out)[i] = o;
-    if (a.mk) a.mk[i] = (unsigned char)pos_bits8(o);
   }
 }
 
@@ -352,24 +249,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
     red[(r0 * C + c0 + e) * 2 + 1] = s2[e];
   }
   __syncthreads();
-  double* slot = acc + (size_t)(blockIdx.x % AVT_BN_SLOTS) * C * 2;
+  bn_write_header(acc, gridDim.x, 0);
+  double* slot = bn_bwd_slots(acc, C) + (size_t)blockIdx.x * C * 2;  // this block's own slot
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float a = 0.f, b = 0.f;
     for (int k = 0; k < rstep; ++k) {
       a += red[(k * C + c) * 2];
       b += red[(k * C + c) * 2 + 1];
     }
-    atomicAdd(slot + 2 * c, (double)a);
-    atomicAdd(slot + 2 * c + 1, (double)b);
+    slot[2 * c] = (double)a;
+    slot[2 * c + 1] = (double)b;
   }
 }
 
-// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2; re-zeroes acc.  16 lanes per
-// channel (as bn_finalize_kernel); lane s of channel c's group.
+// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2 from the slots of workspace acc.
+// 16 lanes per channel (as bn_finalize_kernel); lane s of channel c's group.
 __device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, int s, double inv_rows,
                                                     float* dgamma, float* dbeta, float* k1, float* k2) {
-  const double a = sum16(lane_slots<2>(acc, C, c, s, 0)), b = sum16(lane_slots<2>(acc, C, c, s, 1));
-  lane_slots_zero<2>(acc, C, c, s);
+  double v[2];
+  lane_slots<2>(acc, bn_bwd_slots(acc, C), C, c, s, v);
+  const double a = sum16(v[0]), b = sum16(v[1]);
   if (s != 0) return;
   if (dbeta) dbeta[c] += (float)a;
   if (dgamma) dgamma[c] += (float)b;
@@ -514,7 +413,11 @@ __global__ __launch_bounds__(256) void bn_bwd_mask_reduce_kernel(MaskBwdArgs a) 
     if (TWO) red[(r0 * C + c0 + e) * NS + 2] = s3[e];
   }
   __syncthreads();
-  const size_t slot = (size_t)(blockIdx.x % AVT_BN_SLOTS) * C * 2;
+  bn_write_header(a.acc, gridDim.x, 0);
+  if (TWO) bn_write_header(a.acc2, gridDim.x, 0);
+  const size_t slot = (size_t)blockIdx.x * C * 2;  // this block's own slot
+  double* s1p = bn_bwd_slots(a.acc, C) + slot;
+  double* s2p = TWO ? bn_bwd_slots(a.acc2, C) + slot : nullptr;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float x = 0.f, y = 0.f, z = 0.f;
     for (int k = 0; k < rstep; ++k) {
@@ -522,11 +425,11 @@ __global__ __launch_bounds__(256) void bn_bwd_mask_reduce_kernel(MaskBwdArgs a) 
       y += red[(k * C + c) * NS + 1];
       if (TWO) z += red[(k * C + c) * NS + 2];
     }
-    atomicAdd(a.acc + slot + 2 * c, (double)x);
-    atomicAdd(a.acc + slot + 2 * c + 1, (double)y);
+    s1p[2 * c] = (double)x;
+    s1p[2 * c + 1] = (double)y;
     if (TWO) {
-      atomicAdd(a.acc2 + slot + 2 * c, (double)x);
-      atomicAdd(a.acc2 + slot + 2 * c + 1, (double)z);
+      s2p[2 * c] = (double)x;
+      s2p[2 * c + 1] = (double)z;
     }
   }
 }
@@ -768,51 +671,8 @@ static void bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* 
 
 using namespace avt;
 
-extern "C" size_t avt_bn_acc_doubles(int C) { return (size_t)AVT_BN_SLOTS * C * 3; }
-
-static bool bn_stat_args(const avt_bn_stat* s, int C, BnStatArgs* o) {
-  if (!s) return true;
-  if (!s->acc || !s->gamma || !s->beta || !s->stats || ((uintptr_t)s->acc & 7)) return false;
-  if ((s->running_mean == nullptr) != (s->running_var == nullptr)) return false;
-  o->acc = s->acc;
-  o->gamma = s->gamma;
-  o->beta = s->beta;
-  o->rmean = s->running_mean;
-  o->rvar = s->running_var;
-  o->stats = s->stats;
-  (void)C;
-  return true;
-}
-
-extern "C" int avt_bn_apply_fin(const void* x, const avt_bn_stat* bn, const void* residual, const avt_bn_stat* bn_res,
-                                void* out, void* mask, long long rows, long long rep, int C, int relu, float momentum,
-                                float eps, void* stream) {
-  AVT_REQUIRE(x && bn && out, "bn_apply_fin: null pointer");
-  AVT_REQUIRE(C % 64 == 0 && C <= 2048, "bn_apply_fin: C=%d must be a multiple of 64", C);
-  AVT_REQUIRE(rows > 0 && rep >= 1, "bn_apply_fin: empty input");
-  AVT_REQUIRE(!bn_res || residual, "bn_apply_fin: bn_res without a residual");
-  AVT_REQUIRE(!mask || relu, "bn_apply_fin: mask needs relu");
-  ApplyFinArgs a{};
-  AVT_REQUIRE(bn_stat_args(bn, C, &a.bn) && bn_stat_args(bn_res, C, &a.bnr),
-              "bn_apply_fin: bad avt_bn_stat (null acc/gamma/beta/stats, misaligned acc, or one running stat)");
-  a.x = (const bf16_t*)x;
-  a.res = (const bf16_t*)residual;
-  a.out = (bf16_t*)out;
-  a.mk = (unsigned char*)mask;
-  a.rows = rows;
-  a.rep = rep;
-  a.C = C;
-  a.G = C / 64;
-  a.relu = relu ? 1 : 0;
-  a.momentum = momentum;
-  a.eps = eps;
-  // ~one 256-vector pass per block, at most 1024 blocks (each block's prologue reads 24 KiB of slots)
-  long long pbs = (rows * C / 8 + 255) / 256 / a.G;
-  if (pbs > 1024 / a.G) pbs = 1024 / a.G;
-  if (pbs < 1) pbs = 1;
-  a.nblk = (int)(pbs * a.G);
-  hipLaunchKernelGGL(bn_apply_fin_kernel, dim3(a.nblk), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("bn_apply_fin");
+extern "C" size_t avt_bn_acc_doubles(long long rows, int C) {
+  return rows < 0 || C <= 0 ? 0 : (size_t)kBnHdr + (size_t)bn_slot_cap(rows) * C * 3;
 }
 
 extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta,
@@ -887,9 +747,9 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   }
   hipStream_t st = (hipStream_t)stream;
   double* acc = (double*)t1->workspace;
-  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k1 = (float*)(acc + kBnHdr);
   double* acc2 = t2 ? (double*)t2->workspace : nullptr;
-  float* k1b = t2 ? (float*)(acc2 + (size_t)AVT_BN_SLOTS * C * 2) : nullptr;
+  float* k1b = t2 ? (float*)(acc2 + kBnHdr) : nullptr;
   MaskBwdArgs a{};
   a.g = (const bf16_t*)g;
   a.mk = (const unsigned char*)mask;
@@ -945,10 +805,10 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   return check_launch("bn_bwd_mask");
 }
 
-// workspace: AVT_BN_SLOTS*C*2 doubles (must be zero on entry; left zero on exit) + 2*C floats
+// workspace: header + k1/k2 (2C floats) + the slots of up to `rows` rows (avt_common.h); any contents on entry
 extern "C" size_t avt_bn_bwd_workspace(long long rows, int C) {
-  (void)rows;
-  return (size_t)AVT_BN_SLOTS * C * 2 * sizeof(double) + 2 * (size_t)C * sizeof(float);
+  if (rows < 0 || C <= 0) return 0;
+  return ((size_t)kBnHdr + (size_t)C + (size_t)bn_slot_cap(rows) * C * 2) * sizeof(double);
 }
 
 extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const float* mean, const float* invstd,
@@ -959,7 +819,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   AVT_REQUIRE(rows > 0, "bn_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_bwd: workspace must be 8-byte aligned");
   double* acc = (double*)workspace;
-  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
@@ -974,7 +834,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
 }
 
 // BN backward whose reductions were already accumulated into the workspace by a dgrad epilogue
-// (avt_conv2d_dgrad_bn) over the pre-masked g': finalize (dgamma, dbeta, k1, k2; re-zeroes the
+// (avt_conv2d_dgrad_bn) over the pre-masked g': finalize (dgamma, dbeta, k1, k2 from the
 // accumulator) + apply gc = gamma*invstd*(g' - k1 - xhat*k2).  Same workspace contract as avt_bn_bwd.
 extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float* mean, const float* invstd,
                                     const float* gamma, float* dgamma, float* dbeta, void* gc, void* workspace,
@@ -984,7 +844,7 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   AVT_REQUIRE(rows > 0, "bn_bwd_premasked: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_bwd_premasked: workspace must be 8-byte aligned");
   double* acc = (double*)workspace;
-  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
@@ -1005,7 +865,7 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   AVT_REQUIRE(rows > 0, "bn_relu_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "bn_relu_bwd: workspace must be 8-byte aligned");
   double* acc = (double*)workspace;
-  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
@@ -1048,7 +908,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");
   const int P = (H + 2 - 3) / 2 + 1, Q = (W + 2 - 3) / 2 + 1;
   double* acc = (double*)workspace;
-  float* k1 = (float*)(acc + (size_t)AVT_BN_SLOTS * C * 2);
+  float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,

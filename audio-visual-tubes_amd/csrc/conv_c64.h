@@ -302,12 +302,15 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
       }
   }
   wait_vmcnt<0>();  // drain (the last iteration issued an all-out-of-range half 0)
-  // fp64 atomics per block, not per 256-row tile (~7x fewer at B=128: a conv's queued memory-side
-  // atomics measured ~13-17 us of a layer-1 conv, tools/fin_probe.py)
-  if (MODE == MODE_FWD && p.stats != nullptr && tid < 64 && tlo + jb < thi) {
-    double* a = p.stats + ((size_t)(blockIdx.x % AVT_BN_SLOTS) * p.Ng + tid) * 3;
-    atomicAdd(a + 0, st_s);
-    atomicAdd(a + 1, st_m2);
-    atomicAdd(a + 2, st_r);
+  // BN partials per block (its tiles summed in tile order), stored in the block's own slot (avt_common.h;
+  // a block without tiles stores zeros)
+  if (MODE == MODE_FWD && p.stats != nullptr) {
+    bn_write_header(p.stats, gridDim.x, 0);
+    if (tid < 64) {
+      double* a = bn_fwd_slots(p.stats) + ((size_t)blockIdx.x * p.Ng + tid) * 3;
+      a[0] = st_s;
+      a[1] = st_m2;
+      a[2] = st_r;
+    }
   }
 }

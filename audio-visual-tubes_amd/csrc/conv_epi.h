@@ -144,7 +144,14 @@ __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t
     }
   }
   __syncthreads();
-  const int slot = tile_id % AVT_BN_SLOTS;
+  // this block's own slot (avt_common.h): the call's earlier launches' slots come first (bslot_base), and an
+  // appending call (a stride-2 block's downsample dgrad) starts after the slots of the call before it
+  (void)tile_id;
+  const int total = p.bslot_total ? p.bslot_total : (int)gridDim.x;
+  bn_write_header(p.bacc, total, p.bappend);
+  if (two) bn_write_header(p.bacc2, total, p.bappend);
+  const size_t slot = (size_t)(p.bslot_base + bn_slot_base(p.bacc, p.bappend) + (int)blockIdx.x);
+  const size_t slot2 = two ? (size_t)(p.bslot_base + bn_slot_base(p.bacc2, p.bappend) + (int)blockIdx.x) : 0;
   for (int c = tid; c < BN; c += NT) {
     float a = 0.f, b = 0.f, d = 0.f;
 #pragma unroll
@@ -154,13 +161,13 @@ __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t
       b += q[1];
       d += q[2];
     }
-    double* acc = p.bacc + ((size_t)slot * p.Ng + n0 + c) * 2;
-    atomicAdd(acc, (double)a);
-    atomicAdd(acc + 1, (double)b);
+    double* acc = bn_bwd_slots(p.bacc, p.Ng) + (slot * p.Ng + n0 + c) * 2;
+    acc[0] = (double)a;
+    acc[1] = (double)b;
     if (two) {
-      double* acc2 = p.bacc2 + ((size_t)slot * p.Ng + n0 + c) * 2;
-      atomicAdd(acc2, (double)a);
-      atomicAdd(acc2 + 1, (double)d);
+      double* acc2 = bn_bwd_slots(p.bacc2, p.Ng) + (slot2 * p.Ng + n0 + c) * 2;
+      acc2[0] = (double)a;
+      acc2[1] = (double)d;
     }
   }
 }

@@ -24,9 +24,8 @@ struct GemmNTParams {
   const bf16_t* wmat;  // [Ng][Kg] bf16, K contiguous
   bf16_t* out;         // [M][Ng] bf16
   const bf16_t* add;   // optional [M][Ng] bf16 added to the result (may alias out)
-  double* stats;       // optional BN accumulator [AVT_BN_SLOTS][Ng][3]: per 128-row tile t the fp32
-                       // results' (sum_t, M2_t about the tile mean, sum_t^2/n_t) are added (fp64
-                       // atomics) into slot t % AVT_BN_SLOTS
+  double* stats;       // optional BN accumulator (avt_common.h): per row tile t the fp32 results'
+                       // (sum_t, M2_t about the tile mean, sum_t^2/n_t) are stored into slot t
   int M, Ng, Kg;
   int IH, IW, IC;      // source tensor geometry
   int OH, OW;          // pixel grid of the GEMM rows
@@ -37,7 +36,8 @@ struct GemmNTParams {
   // result g (after `add`) is masked by the ReLU of the BN that produced the positions' activations,
   // g' = g * [by > 0] (by given: the block output) or g * [fma(bx, scale, shift) > 0] (BasicBlock.bn1),
   // stored as g', and that BN's backward reductions (sum g', sum g' * xhat), xhat = (bx - mean)*invstd,
-  // are added (fp64 atomics) into bacc [AVT_BN_SLOTS][Ng][2]; bx2/bst2/bacc2 optionally a second BN fed
+  // are stored into slot bslot_base (+ bacc's header[0] when bappend) + blockIdx.x of bacc (avt_common.h;
+  // bslot_total: the slots of all launches of this call, 0 = gridDim.x); bx2/bst2/bacc2 optionally a second BN fed
   // by the same g' (the downsample BN of a first block: bn2 and downsample.1 share the ReLU).
   const bf16_t* bx;
   const bf16_t* by;
@@ -48,6 +48,7 @@ struct GemmNTParams {
   double* bacc2;
   int bskip00;         // host side: a stride-2 dgrad's class-(0,0) launch stores plain g (another
                        // kernel -- the downsample dgrad -- adds to those pixels and applies the epilogue)
+  int bslot_base, bslot_total, bappend;
   const unsigned char* amask;  // optional [M][Ng/8] bits: `add` enters masked, add * bit (an identity
                                // block's residual gradient g * [out > 0], from avt_bn_apply_mask's bits)
 };
@@ -248,14 +249,15 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
       (void)colsum;
     }
     __syncthreads();
-    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
+    bn_write_header(p.stats, (p.M + BM - 1) / BM, 0, mt == 0 && n0 == 0);
+    double* acc_slot = bn_fwd_slots(p.stats) + (size_t)mt * p.Ng * 3;  // this row tile's own slot
     for (int c = tid; c < BN; c += 256) {
       const double s = (double)red[c] + (double)red[BN + c];
       const double m2 = (double)red[2 * BN + c] + (double)red[3 * BN + c];
       double* a = acc_slot + (size_t)(n0 + c) * 3;
-      atomicAdd(a + 0, s);
-      atomicAdd(a + 1, m2);
-      atomicAdd(a + 2, s * s / (double)rows_valid);
+      a[0] = s;
+      a[1] = m2;
+      a[2] = s * s / (double)rows_valid;
     }
   }
 
@@ -511,7 +513,9 @@ static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64
 static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
 static int g_wgrad_blocks = 0;     // wgrad split-K: 0 = wave model (wgrad_plan), >0 = fixed block target
 static int g_wgrad_min_kt = 4;
-static int g_wgrad_slab_max = 32;  // largest split count that goes through a slab
+// largest split count that goes through a slab (deterministic: split partials summed in split order); beyond it
+// fp32 atomics (non-deterministic summation order; an A/B knob only: AVT_WGRAD_SLAB_MAX / avt_set_wgrad_slab_max)
+static int g_wgrad_slab_max = 1 << 30;
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
@@ -784,31 +788,45 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
     launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
     return;
   }
-  for (int ph = 0; ph < 2; ++ph)
-    for (int pw = 0; pw < 2; ++pw) {
-      NTPipeArgsV tc = ta;
-      tc.ph = ph;
-      tc.pw = pw;
-      tc.ntaps = 0;
-      for (int r = 0; r < p.R; ++r)
-        for (int s = 0; s < p.S; ++s) {
-          if (((ph + p.pad - r) & 1) || ((pw + p.pad - s) & 1)) continue;
-          tc.tap_w[tc.ntaps] = r * p.S + s;
-          tc.tap_dy[tc.ntaps] = (ph + p.pad - r) / 2;
-          tc.tap_dx[tc.ntaps] = (pw + p.pad - s) / 2;
-          ++tc.ntaps;
+  // the class launches that carry the BN-backward epilogue store their partial sums into consecutive
+  // slot ranges of one accumulator (conv_epi.h): pass 0 counts the call's slots, pass 1 launches
+  constexpr int BMc = WM * TM * 32, BNc = WN * TN * 32;
+  int ep_total = 0, ep_base = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        NTPipeArgsV tc = ta;
+        tc.ph = ph;
+        tc.pw = pw;
+        tc.ntaps = 0;
+        for (int r = 0; r < p.R; ++r)
+          for (int s = 0; s < p.S; ++s) {
+            if (((ph + p.pad - r) & 1) || ((pw + p.pad - s) & 1)) continue;
+            tc.tap_w[tc.ntaps] = r * p.S + s;
+            tc.tap_dy[tc.ntaps] = (ph + p.pad - r) / 2;
+            tc.tap_dx[tc.ntaps] = (pw + p.pad - s) / 2;
+            ++tc.ntaps;
+          }
+        GemmNTParams pc = p;
+        if (p.bskip00 && ph == 0 && pw == 0) pc.bx = pc.bx2 = nullptr;
+        pc.OH = (p.OH - ph + 1) / 2;
+        pc.OW = (p.OW - pw + 1) / 2;
+        pc.M = batch * pc.OH * pc.OW;
+        // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) runs with an empty
+        // K loop: its rows are written as 0 (+ add) -- or, accumulating in place (add == out), are
+        // already final and are skipped
+        if (tc.ntaps == 0 && p.add != nullptr && p.add == p.out) continue;
+        const int grid = ((pc.M + BMc - 1) / BMc) * (p.Ng / BNc);
+        if (grid <= 0) continue;
+        if (pass == 0) {
+          if (pc.bx != nullptr) ep_total += grid;
+          continue;
         }
-      GemmNTParams pc = p;
-      if (p.bskip00 && ph == 0 && pw == 0) pc.bx = pc.bx2 = nullptr;
-      pc.OH = (p.OH - ph + 1) / 2;
-      pc.OW = (p.OW - pw + 1) / 2;
-      pc.M = batch * pc.OH * pc.OW;
-      // a class no tap reaches (e.g. 3 of the 4 classes of a 1x1/s2 downsample) runs with an empty
-      // K loop: its rows are written as 0 (+ add) -- or, accumulating in place (add == out), are
-      // already final and are skipped
-      if (tc.ntaps == 0 && p.add != nullptr && p.add == p.out) continue;
-      launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
-    }
+        pc.bslot_base = ep_base;
+        pc.bslot_total = ep_total;
+        if (pc.bx != nullptr) ep_base += grid;
+        launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
+      }
 }
 
 constexpr int kHaloPR = 416;  // patch rows the halo kernels' LDS holds: 256 + 2W + 2 <= 416 -> W <= 79
@@ -1091,7 +1109,6 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
   hipLaunchKernelGGL((gemm_nt_kernel<MODE, CVEC, BM, BN>), dim3(grid), dim3(256), 0, st, p);
 }
 
-extern "C" int avt_bn_slots(void) { return AVT_BN_SLOTS; }
 
 static int conv2d_fwd_impl(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp,
                            int K, int R, int S, int stride, int pad, int Kg, const SplitWs* ws, void* stream);
@@ -1251,6 +1268,7 @@ static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const voi
     p.bst2 = epi->stats2;
     p.bacc2 = epi->acc2;
     p.bskip00 = epi->skip_class00;
+    p.bappend = epi->append_slots ? 1 : 0;
   }
   hipStream_t st = (hipStream_t)stream;
   if (C % 128 == 0)

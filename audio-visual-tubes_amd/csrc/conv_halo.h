@@ -380,7 +380,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       if (lane < FR) red[WM * BN + wm * BN + cc] = q;
     }
     __syncthreads();
-    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
+    // this row tile's own slot (avt_common.h): (M + BM - 1) / BM slots, plain stores
+    bn_write_header(p.stats, (p.M + BM - 1) / BM, 0, mt == 0 && n0 == 0);
+    double* acc_slot = bn_fwd_slots(p.stats) + (size_t)mt * p.Ng * 3;
     for (int cc = tid; cc < BN; cc += NT) {
       double sd = 0.0, m2 = 0.0;
 #pragma unroll
@@ -389,9 +391,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         m2 += (double)red[WM * BN + k * BN + cc];
       }
       double* a = acc_slot + (size_t)(n0 + cc) * 3;
-      atomicAdd(a + 0, sd);
-      atomicAdd(a + 1, m2);
-      atomicAdd(a + 2, sd * sd / (double)rows_valid);
+      a[0] = sd;
+      a[1] = m2;
+      a[2] = sd * sd / (double)rows_valid;
     }
   }
   bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);

@@ -341,7 +341,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
       if (lane < 32) red[WM * BN + wm * BN + c] = q;
     }
     __syncthreads();
-    double* acc_slot = p.stats + (size_t)(mt % AVT_BN_SLOTS) * p.Ng * 3;
+    // this row tile's own slot (avt_common.h): (M + BM - 1) / BM slots, plain stores
+    bn_write_header(p.stats, (p.M + BM - 1) / BM, 0, mt == 0 && n0 == 0);
+    double* acc_slot = bn_fwd_slots(p.stats) + (size_t)mt * p.Ng * 3;
     for (int c = tid; c < BN; c += NT) {
       double s = 0.0, m2 = 0.0;
 #pragma unroll
@@ -350,9 +352,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
         m2 += (double)red[WM * BN + k * BN + c];
       }
       double* a = acc_slot + (size_t)(n0 + c) * 3;
-      atomicAdd(a + 0, s);
-      atomicAdd(a + 1, m2);
-      atomicAdd(a + 2, s * s / (double)rows_valid);
+      a[0] = s;
+      a[1] = m2;
+      a[2] = s * s / (double)rows_valid;
     }
   }
   bf16_t* Ct = reinterpret_cast<bf16_t*>(smem);

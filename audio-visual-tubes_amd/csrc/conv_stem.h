@@ -1,7 +1,7 @@
 // 7x7 / stride 2 / pad 3 stem convolutions (models/base_models.py:135-138: the vision conv1 over
 // 3 channels padded to 4, the audio conv1_a over 1 channel), 64 output channels, forward with the BN
 // partial statistics of the other forward kernels.  Included by conv_gemm.hip inside namespace avt
-// (needs AVT_BN_SLOTS, f2bf).
+// (needs the BN accumulator helpers of avt_common.h, f2bf).
 //
 // The stem is store-bound: 64 bf16 channels out per output pixel (205 MB vision / 317 MB audio at
 // B = 128 against 51 / 20 MB of input), and the first versions of this kernel were VALU-bound on
@@ -33,7 +33,7 @@
 //     one channel as ds_write_b64 into [64 ch][32 px], back with ds_read_b64_tr_b16 as 8-channel
 //     16-byte chunks of one pixel, 16-byte global stores;
 //   * at the end each wave's (n, sum, M2 = sumsq - sum^2/n) merge (Chan, fp64) in LDS and each block
-//     adds (sum, M2, sum^2/n) into slot blockIdx % AVT_BN_SLOTS (the format avt_bn_finalize merges).
+//     stores (sum, M2, sum^2/n) into slot blockIdx (the format avt_bn_finalize merges).
 #pragma once
 
 // orders a wave's own LDS writes before its later LDS reads of them (other lanes' data): a
@@ -48,7 +48,7 @@ struct StemArgs {
   const bf16_t* x;  // [N][IH][IW][C]
   const bf16_t* w;  // [64][Kg], k' = (r*7+s)*C + c
   bf16_t* y;        // [N][OH][OW][64]
-  double* stats;    // optional [AVT_BN_SLOTS][64][3]
+  double* stats;    // optional BN accumulator (avt_common.h): one slot per block
   unsigned x_bytes, y_bytes;
   int N, IH, IW, OH, OW, Kg;
   int tiles_per_row, total_tiles;
@@ -275,6 +275,7 @@ __global__ __launch_bounds__(kStemNW * 64, 1) void conv_stem_fwd_kernel(StemArgs
 
   // ---- per-wave (n, sum, M2) -> LDS, Chan merge over the waves, publish ----
   if (a.stats != nullptr) {
+    bn_write_header(a.stats, gridDim.x, 0);
     // channel frow of j: sum in dsum row 4 fhalf (j = 0) / 16 + 4 fhalf (j = 1) of column frow;
     // sumsq on the diagonal (row frow), held by the lane with fhalf = (frow >> 2) & 1
     const int vd = (frow & 3) + 4 * (frow >> 3);
@@ -314,12 +315,10 @@ __global__ __launch_bounds__(kStemNW * 64, 1) void conv_stem_fwd_kernel(StemArgs
         s += q[1];
         n += nb;
       }
-      if (n > 0.0) {
-        double* slot = a.stats + ((size_t)(blockIdx.x % AVT_BN_SLOTS) * 64 + tid) * 3;
-        atomicAdd(slot + 0, s);
-        atomicAdd(slot + 1, m2);
-        atomicAdd(slot + 2, s * s / n);
-      }
+      double* slot = bn_fwd_slots(a.stats) + ((size_t)blockIdx.x * 64 + tid) * 3;  // this block's own slot
+      slot[0] = s;
+      slot[1] = m2;
+      slot[2] = n > 0.0 ? s * s / n : 0.0;
     }
   }
 }

@@ -66,8 +66,8 @@ __global__ __launch_bounds__(256) void vis_norm_kernel(const T* __restrict__ v, 
 // ---- small fp32 GEMM with strided operands ----
 //   C[m][n] (+)= rowscale[m] * sum_k A(m,k) * kscale[k] * B(k,n)
 //   A(m,k) = a[m*sam + k*sak] (TA = bf16_t or float), B(k,n) = b[k*sbk + n*sbn] (TB)
-//   split-K over gridDim.z with fp32 atomics when gridDim.z > 1 (C pre-zeroed by caller, or holding
-//   what to add to); accum = 1 adds to C in the single-split case too.
+//   split-K over gridDim.z: split z stores its partial product into c + z * M * ldc (a workspace), which
+//   sgemm_sum_splits_kernel then sums in split order into the output (deterministic); accum = 1 adds to C.
 // 64x64 block tile, 32-deep k-tiles staged through LDS as fp32; four waves each own a 32x32 quarter
 // on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: full fp32 products and fp32 accumulation, as
 // the reference's fp32 einsum -- only the summation order differs), 16 MFMAs per k-tile.  Each
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
     if (gm >= M || gn >= N) continue;
     const float r = acc[v] * (rowscale ? rowscale[gm] : 1.f);
     if (gridDim.z > 1)
-      atomicAdd(c + (size_t)gm * ldc + gn, r);
+      c[(size_t)blockIdx.z * M * ldc + (size_t)gm * ldc + gn] = r;
     else if (accum)
       c[(size_t)gm * ldc + gn] += r;
     else
@@ -640,16 +640,40 @@ __global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, in
   if (i < n) p[i] = 0.f;
 }
 
+// out[i] (+)= sum over s = 0 .. splits-1 of part[s * n + i], in that order
+__global__ __launch_bounds__(256) void sgemm_sum_splits_kernel(const float* __restrict__ part, int splits, long long n,
+                                                               float* __restrict__ out, int accum) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < splits; ++s) v += part[s * n + i];
+    out[i] = accum ? out[i] + v : v;
+  }
+}
+
+// split-K partials of the head GEMMs: at most kSgSplits splits of an M x N output
+constexpr int kSgSplits = 64;
+
+// C = ... with up to `splits` k-splits; ws: kSgSplits * M * N floats for the split partials (NULL: one split)
 template <typename TA, typename TB>
 static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak, const TB* b, long long sbk,
                   long long sbn, const float* rowscale, const float* kscale, float* c, long long ldc, int splits,
-                  hipStream_t st, int accum = 0) {
+                  hipStream_t st, int accum = 0, float* ws = nullptr) {
+  if (ws == nullptr) splits = 1;
+  if (splits > kSgSplits) splits = kSgSplits;
   int kps = (K + splits - 1) / splits;
   kps = ((kps + kSgKT - 1) / kSgKT) * kSgKT;
   splits = (K + kps - 1) / kps;
   dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
-  hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
-                     kscale, c, ldc, kps, accum);
+  if (splits > 1) {
+    hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
+                       kscale, ws, (long long)N, kps, 0);
+    const long long n = (long long)M * N;  // ldc == N here (the head's outputs are dense)
+    hipLaunchKernelGGL(sgemm_sum_splits_kernel, dim3((unsigned)min(2048LL, (n + 255) / 256)), dim3(256), 0, st, ws,
+                       splits, n, c, accum);
+  } else {
+    hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
+                       kscale, c, ldc, kps, accum);
+  }
 }
 
 }  // namespace avt
@@ -657,6 +681,8 @@ static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak
 using namespace avt;
 
 extern "C" size_t avt_hardway_save_floats(int B) { return (size_t)B * (2 * B + 4); }
+
+extern "C" size_t avt_hardway_bwd_ws_floats(int B, int C) { return B > 0 && C > 0 ? (size_t)kSgSplits * B * C : 0; }
 
 // Forward of the hard-way head from the trunk outputs.
 //   v [B][P][C] bf16, an [B][C] fp32 (unit audio vectors)
@@ -697,7 +723,7 @@ extern "C" int avt_hardway_bwd_ex(const void* v, const float* an, const float* i
                                   const float* save, const float* dlogits, int B, int P, int C, float eps1, float eps2,
                                   float tau, int trimap, int use_neg, const float* dwA, const float* vsum, float* dm,
                                   const float* gA, const float* gPos, const float* gNeg, float* dA0, float* dvh,
-                                  void* gv, float* gan, int gan_accumulate, void* stream) {
+                                  void* gv, float* gan, int gan_accumulate, float* ws, void* stream) {
   AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && gan, "hardway_bwd: null pointer");
   AVT_REQUIRE((dvh == nullptr) == (gv == nullptr), "hardway_bwd: dvh and gv must be both set or both null");
   AVT_REQUIRE(dwA == nullptr || (vsum && dm && gv), "hardway_bwd: dwA needs vsum, dm and the vision gradient");
@@ -715,14 +741,12 @@ extern "C" int avt_hardway_bwd_ex(const void* v, const float* an, const float* i
   // dvh[(i,p)][c] = sum_j dA0[(i,p)][j] * an[j][c]   (skipped when the vision map is detached:
   // the tube head, whose video features come from a detached forward hook, model.py:12-15)
   if (gv != nullptr) sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
-  // gan[j][c] (+)= sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]
-  // zeroed by a kernel, not hipMemsetAsync: a memset node in a replayed segment graph was observed to
-  // race the kernel after it (tools/diag_seg2.py: garbage gan in ~half of the replays)
-  if (!gan_accumulate) hipLaunchKernelGGL(zero_f32_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, gan, B * C);
+  // gan[j][c] (+)= sum_{(i,p)} dA0[(i,p)][j] * inv[(i,p)] * v[(i,p)][c]: split-K over the B*P rows through the
+  // ws partials, summed in split order (deterministic)
   int splits = rows / 256;
   if (splits < 1) splits = 1;
-  if (splits > 64) splits = 64;
-  sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st, 1);
+  sgemm<float, bf16_t>(B, C, rows, dA0, 1, B, (const bf16_t*)v, C, 1, nullptr, inv, gan, C, splits, st,
+                       gan_accumulate, ws);
   if (gv != nullptr)
     hipLaunchKernelGGL((vis_norm_bwd_kernel<bf16_t, true>), dim3((rows + 3) / 4), dim3(256), 0, st, (const bf16_t*)v,
                        inv, dvh, dwA != nullptr ? dm : nullptr, (bf16_t*)gv, rows, C);
@@ -734,7 +758,7 @@ extern "C" int avt_hardway_bwd(const void* v, const float* an, const float* inv,
                                int use_neg, const float* dwA, const float* vsum, float* dm, float* dA0, float* dvh,
                                void* gv, float* gan, int gan_accumulate, void* stream) {
   return avt_hardway_bwd_ex(v, an, inv, A0, save, dlogits, B, P, C, eps1, eps2, tau, trimap, use_neg, dwA, vsum, dm,
-                            nullptr, nullptr, nullptr, dA0, dvh, gv, gan, gan_accumulate, stream);
+                            nullptr, nullptr, nullptr, dA0, dvh, gv, gan, gan_accumulate, nullptr, stream);
 }
 
 // Standalone HardWayAttention (model.py:38-60): the head on fp32 features taken as given (no
@@ -762,7 +786,7 @@ extern "C" int avt_hardway_attention_fwd(const float* v, const float* an, int B,
 extern "C" int avt_hardway_attention_bwd(const float* v, const float* an, const float* inv, const float* A0,
                                          const float* save, const float* dlogits, const float* gA, int B, int P,
                                          int C, float eps1, float eps2, float tau, float* dA0, float* dvh, float* gv,
-                                         float* gan, void* stream) {
+                                         float* gan, float* ws, void* stream) {
   AVT_REQUIRE(v && an && inv && A0 && save && dlogits && dA0 && dvh && gv && gan,
               "hardway_attention_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && B >= 1 && P >= 1, "hardway_attention_bwd: bad shape B=%d P=%d C=%d", B, P, C);
@@ -775,11 +799,9 @@ extern "C" int avt_hardway_attention_bwd(const float* v, const float* an, const 
     hipLaunchKernelGGL(hardway_aux_bwd_kernel, dim3((rows + 255) / 256), dim3(256), 0, st, A0, gA, nullptr, nullptr,
                        B, P, eps1, eps2, tau, 1, dA0);
   sgemm<float, float>(rows, C, B, dA0, B, 1, an, C, 1, nullptr, nullptr, dvh, C, 1, st);
-  hipLaunchKernelGGL(zero_f32_kernel, dim3((B * C + 255) / 256), dim3(256), 0, st, gan, B * C);
   int splits = rows / 256;
   if (splits < 1) splits = 1;
-  if (splits > 64) splits = 64;
-  sgemm<float, float>(B, C, rows, dA0, 1, B, v, C, 1, nullptr, nullptr, gan, C, splits, st, 1);
+  sgemm<float, float>(B, C, rows, dA0, 1, B, v, C, 1, nullptr, nullptr, gan, C, splits, st, 0, ws);
   hipLaunchKernelGGL((vis_norm_bwd_kernel<float, false>), dim3((rows + 3) / 4), dim3(256), 0, st, v, inv, dvh,
                      nullptr, gv, rows, C);
   return check_launch("hardway_attention_bwd");

@@ -211,15 +211,8 @@ class _EngineStore(Store):
     def packed(self, spec):
         return self.e.packs[spec.name]
 
-    def stat_acc(self, bn, kind):
-        return self.e.stat_views[(bn.prefix, kind)]
-
-    def zero_stats(self, trunk):
-        z = self.e._stat_trunk.get(trunk.prefix)
-        if z is None:
-            return False
-        z.zero_()
-        return True
+    def stat_acc(self, bn, kind, rows):
+        return self.e.stat_acc(bn, kind, rows)
 
     def splitk(self, spec, dgrad, N, H, W):
         return self.e.splitk_ws(spec, dgrad, N, H, W)
@@ -236,8 +229,8 @@ class AVEngine:
         self.packs: Dict[str, Tuple[torch.Tensor, Optional[torch.Tensor]]] = {}
         self._pack_table = None
         self._pack_max = 0
-        self.stat_views: Dict = {}
-        self._stat_arena = None
+        self.stat_views: Dict = {}  # (BN prefix, 'fwd' | 'bwd') -> its statistics accumulator
+        self._retired: List[torch.Tensor] = []
         self._alloc(flat.flat.device)
         # run the audio trunk on a second HIP stream, concurrently with the vision trunk (forward and
         # backward): the two trunks are independent until the head, and their kernels fill each
@@ -355,22 +348,31 @@ class AVEngine:
             blob = b"".join(descs)
             self._pack_table = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
         self._pack_n, self._pack_max = len(descs), maxel
-        # BN accumulators: per BN 'fwd' [slots][C][3] f64 and 'bwd' [slots][C][2] f64 + k1/k2 (2C f32)
-        slots = int(query("avt_bn_slots"))
-        offs, total = {}, 0
-        spans = {}  # trunk prefix -> its accumulators' contiguous region of the arena
-        for tr in self.bn_trunks:
-            first = total
-            for bn in tr.bns():
-                n_f = int(query("avt_bn_acc_doubles", bn.c))  # [slots][C][3]
-                n_b = slots * bn.c * 2 + bn.c  # + 2C floats == C doubles
-                offs[(bn.prefix, "fwd")] = (total, n_f)
-                offs[(bn.prefix, "bwd")] = (total + n_f, n_b)
-                total += n_f + n_b
-            spans[tr.prefix] = (first, total)
-        self._stat_arena = torch.zeros(total, device=dev, dtype=torch.float64)
-        self.stat_views = {k: self._stat_arena[o:o + n] for k, (o, n) in offs.items()}
-        self._stat_trunk = {p: self._stat_arena[a:b] for p, (a, b) in spans.items()}
+
+    def head_ws(self, B: int, C: int) -> torch.Tensor:
+        """Split-K partials of the head backward's audio-vector GEMM (avt_hardway_bwd_ws_floats)."""
+        n = int(query("avt_hardway_bwd_ws_floats", B, C))
+        t = getattr(self, "_head_ws", None)
+        if t is None or t.numel() < n:
+            if t is not None:
+                self._retired.append(t)
+            t = self._head_ws = torch.empty(n, device=self.flat.flat.device, dtype=torch.float32)
+        return t
+
+    def stat_acc(self, bn, kind: str, rows: int) -> torch.Tensor:
+        """A BN's fp64 statistics accumulator for `rows` rows (include/avt.h "BatchNorm statistics": the
+        producing kernel overwrites its slots, no zeroing), kept per (BN, kind) and grown when a larger batch
+        comes: a captured graph keeps the tensor it was captured with alive through this dict."""
+        key = (bn.prefix, kind)
+        need = int(query("avt_bn_acc_doubles", rows, bn.c)) if kind == "fwd" else \
+            (int(query("avt_bn_bwd_workspace", rows, bn.c)) + 7) // 8
+        t = self.stat_views.get(key)
+        if t is None or t.numel() < need:
+            if t is not None:
+                self._retired.append(t)  # a graph captured on it may still replay
+            t = torch.empty(need, device=self.flat.flat.device, dtype=torch.float64)
+            self.stat_views[key] = t
+        return t
 
     # ----------------------------------------------------------------------------- weights
     def pack_weights(self):
@@ -525,7 +527,7 @@ class AVEngine:
         call("avt_hardway_bwd_ex", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
              P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, int(self.tri_map), int(self.neg), P(dwA),
              P(tape["vsum"] if dwA is not None else None), P(dm), P(aux[0]), P(aux[1]), P(aux[2]), P(dA0), P(dvh),
-             P(gv), P(gan), int(accumulate), stream_ptr())
+             P(gv), P(gan), int(accumulate), P(self.head_ws(B, C)), stream_ptr())
         return gv, gan
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,

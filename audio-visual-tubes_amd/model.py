@@ -434,8 +434,9 @@ class _HardWayAttentionFunction(torch.autograd.Function):
         dA0, dvh, gv = torch.empty(B, Pn, B, **f32), torch.empty(B, Pn, C, **f32), torch.empty(B, Pn, C, **f32)
         gan = torch.empty(B, C, **f32)
         eps1, eps2, tau = ctx.hp
+        ws = torch.empty(int(query("avt_hardway_bwd_ws_floats", B, C)), **f32)
         call("avt_hardway_attention_bwd", P(v), P(an), P(inv), P(A0), P(save), P(dl), P(ga), B, Pn, C, eps1, eps2,
-             tau, P(dA0), P(dvh), P(gv), P(gan), stream_ptr())
+             tau, P(dA0), P(dvh), P(gv), P(gan), P(ws), stream_ptr())
         g_vid = gv.view(b, t, h, w, C).permute(0, 4, 1, 2, 3).to(ctx.dtypes[1])
         return gan.to(ctx.dtypes[0]), g_vid, None, None, None
 

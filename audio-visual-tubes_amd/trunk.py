@@ -15,7 +15,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ._lib import BnBwdTarget, BnStat, DgradBnEpi, call, query
+from ._lib import BnBwdTarget, DgradBnEpi, call, query
 
 STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
 # 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
@@ -128,14 +128,11 @@ class Store:
     def buffer(self, name: str) -> torch.Tensor: ...
     def grad(self, name: str) -> Optional[torch.Tensor]: ...
     def packed(self, spec: ConvSpec): ...
-    def stat_acc(self, bn: "BNSpec", kind: str) -> torch.Tensor:
-        """Zeroed fp64 accumulator for a BN ('fwd': avt_bn_acc_doubles(C); 'bwd': bn_bwd workspace)."""
+    def stat_acc(self, bn: "BNSpec", kind: str, rows: int) -> torch.Tensor:
+        """fp64 statistics accumulator of a BN over `rows` rows ('fwd': avt_bn_acc_doubles(rows, C) doubles;
+        'bwd': the avt_bn_bwd_workspace(rows, C) workspace).  Any contents (the producers overwrite their
+        slots); the same tensor for a BN's producer and its consumer within a step."""
         ...
-
-    def zero_stats(self, trunk: "Trunk") -> bool:
-        """Zero all of trunk's BN accumulators (stat_acc) in one launch; False if this store cannot (the
-        trunk then finalizes in separate launches, which re-zero them)."""
-        return False
 
     def splitk(self, spec: "ConvSpec", dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) split-K workspace of this conv call (avt_conv2d_splitk_plan), or None."""
@@ -177,9 +174,6 @@ class Trunk:
         self.prefix, self.modal = prefix, modal
         self.bn_rep = 1  # >1: each input sample stands for bn_rep identical ones (tube audio de-dup)
         self.bn_momentum = 0.1  # 0.19: two reference forwards over the same batch in one (two-view audio)
-        # train mode: BN finalize inside the apply launch (avt_bn_apply_fin; AVT_BN_FIN=1).  Off by default:
-        # -1 % at B=32 and B=128 against separate finalize launches (tools/r3_binfin.sh)
-        self.bn_fin = os.environ.get("AVT_BN_FIN", "0") == "1"
         if modal == "audio":
             self.stem = ConvSpec(prefix + "conv1_a.weight", 1, 64, 7, 2, 3, 1)
         else:
@@ -219,12 +213,11 @@ class Trunk:
         return out
 
     # ------------------------------------------------------------------ forward
-    def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool, finalize: bool = True):
-        """conv + its BN statistics; finalize=False (training): returns the accumulator in place of the
-        stats, for _bn_apply_fin to finalize in the consuming launch."""
+    def _conv_bn(self, x, N, H, W, spec: ConvSpec, bn: BNSpec, store: Store, training: bool):
+        """conv + its BN statistics (finalized: stats [4, C])."""
         Pq, Qq = conv_out(H, spec.k, spec.stride, spec.pad), conv_out(W, spec.k, spec.stride, spec.pad)
         y = torch.empty(N, Pq, Qq, spec.cout, device=x.device, dtype=torch.bfloat16)
-        acc = store.stat_acc(bn, "fwd") if training else None
+        acc = store.stat_acc(bn, "fwd", N * Pq * Qq) if training else None
         wf, _ = store.packed(spec)
         ws = store.splitk(spec, False, N, H, W)
         ev = ConvProfiler.begin()
@@ -236,33 +229,8 @@ class Trunk:
                  spec.stride, spec.pad, spec.kg, stream_ptr())
         ConvProfiler.end(ev, "fwd", 2.0 * N * Pq * Qq * spec.cout * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + wf.numel() + y.numel()))
-        if not finalize:
-            return y, acc, Pq, Qq
         stats = _bn_finalize(y, acc, N * Pq * Qq, bn, store, training, momentum=self.bn_momentum, rep=self.bn_rep)
         return y, stats, Pq, Qq
-
-    def _bn_apply_fin(self, c, acc, bn: BNSpec, store: Store, res=None, res_acc=None, res_bn=None, mask=None,
-                      eps=1e-5):
-        """Train mode: finalize bn (and res_bn) from their accumulators + apply (+residual) + ReLU in one
-        launch (avt_bn_apply_fin); returns (out, stats[4,C], res_stats[4,C] or None)."""
-        C = c.shape[-1]
-        rows = c.numel() // C
-
-        def stat(b, a):
-            st = torch.empty(4, C, device=c.device, dtype=torch.float32)
-            d = BnStat()
-            d.acc, d.stats = a.data_ptr(), st.data_ptr()
-            d.gamma, d.beta = store.param(b.prefix + ".weight").data_ptr(), store.param(b.prefix + ".bias").data_ptr()
-            d.running_mean = store.buffer(b.prefix + ".running_mean").data_ptr()
-            d.running_var = store.buffer(b.prefix + ".running_var").data_ptr()
-            return st, d
-
-        s, d = stat(bn, acc)
-        sr, dr = stat(res_bn, res_acc) if res_bn is not None else (None, None)
-        out = torch.empty_like(c)
-        call("avt_bn_apply_fin", P(c), ctypes.byref(d), P(res), ctypes.byref(dr) if dr is not None else None, P(out),
-             P(mask), rows, self.bn_rep, C, 1, ctypes.c_float(self.bn_momentum), ctypes.c_float(eps), stream_ptr())
-        return out, s, sr
 
     def forward(self, x: torch.Tensor, store: Store, training: bool, io: Optional[Dict] = None):
         """x: [N,H,W,cp] bf16 NHWC. Returns (layer4 map [N,h,w,512] bf16, tape).  io (optional) receives
@@ -274,8 +242,6 @@ class Trunk:
         be issued interleaved on two streams (engine._interleave); returns forward()'s result."""
         N, H, W, _ = x.shape
         tape: Dict = {"x": x, "N": N, "H": H, "W": W, "blocks": []}
-        # this trunk's BN accumulators zeroed (one launch): avt_bn_apply_fin leaves its inputs unzeroed
-        zeroed = training and store.zero_stats(self)
         c0, st0, H1, W1 = self._conv_bn(x, N, H, W, self.stem, self.bn1, store, training)
         yield
         # bn1 -> relu -> maxpool fused: the full-resolution relu(bn1(c0)) is never stored
@@ -288,31 +254,10 @@ class Trunk:
         tape.update(c0=c0, st0=st0, idx=idx, carg=carg, H1=H1, W1=W1)
         yield
         cur, Hc, Wc = p0, H2, W2
-        fuse = training and self.bn_fin and zeroed
         for bi, blk in enumerate(self.blocks):
             if io is not None and bi == 6:
                 io["layer4_in"] = cur
             t = {"x": cur, "H": Hc, "W": Wc}
-            if fuse:  # finalize folded into the apply launches (avt_bn_apply_fin)
-                c1, a1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training, False)
-                yield
-                h1, s1, _ = self._bn_apply_fin(c1, a1, blk["bn1"], store)
-                yield
-                c2, a2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training, False)
-                yield
-                om = torch.empty(c2.numel() // 8, device=x.device, dtype=torch.uint8)
-                if blk["down"] is not None:
-                    cd, ad, _, _ = self._conv_bn(cur, N, Hc, Wc, blk["down"], blk["bnd"], store, training, False)
-                    yield
-                    out, s2, sd = self._bn_apply_fin(c2, a2, blk["bn2"], store, cd, ad, blk["bnd"], om)
-                    t.update(cd=cd, sd=sd)
-                else:
-                    out, s2, _ = self._bn_apply_fin(c2, a2, blk["bn2"], store, cur, mask=om)
-                t.update(c1=c1, s1=s1, h1=h1, c2=c2, s2=s2, out=out, om=om, Ho=Ho, Wo=Wo)
-                tape["blocks"].append(t)
-                yield
-                cur, Hc, Wc = out, Ho, Wo
-                continue
             c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
             yield
             h1 = torch.empty_like(c1)
@@ -350,7 +295,7 @@ class Trunk:
     def _bn_bwd(self, g, y, xc, stats, bn: BNSpec, store: Store, gmask_out=None):
         rows = xc.numel() // bn.c
         gc = torch.empty_like(xc)
-        ws = store.stat_acc(bn, "bwd")
+        ws = store.stat_acc(bn, "bwd", rows)
         call("avt_bn_bwd", P(g), P(y), P(xc), P(stats[2]), P(stats[3]), P(store.param(bn.prefix + ".weight")),
              P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc), P(gmask_out), P(ws),
              rows, bn.c, stream_ptr())
@@ -365,7 +310,7 @@ class Trunk:
         t.dgamma = dg.data_ptr() if dg is not None else None
         t.dbeta = db.data_ptr() if db is not None else None
         t.gc = gc.data_ptr()
-        t.workspace = store.stat_acc(bn, "bwd").data_ptr()
+        t.workspace = store.stat_acc(bn, "bwd", xc.numel() // bn.c).data_ptr()
         t.keep = gc  # the output tensor (ctypes.Structure keeps no reference)
         return t
 
@@ -382,7 +327,7 @@ class Trunk:
         """bn -> relu backward with the mask recomputed from (xc, scale, shift) (BasicBlock.bn1)."""
         rows = xc.numel() // bn.c
         gc = torch.empty_like(xc)
-        ws = store.stat_acc(bn, "bwd")
+        ws = store.stat_acc(bn, "bwd", rows)
         call("avt_bn_relu_bwd", P(g), P(xc), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]),
              P(store.param(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".weight")),
              P(store.grad(bn.prefix + ".bias")), P(gc), P(ws), rows, bn.c, stream_ptr())
@@ -441,17 +386,21 @@ class Trunk:
         gc = torch.empty_like(xc)
         call("avt_bn_bwd_premasked", P(gm), P(xc), P(stats[2]), P(stats[3]), P(store.param(bn.prefix + ".weight")),
              P(store.grad(bn.prefix + ".weight")), P(store.grad(bn.prefix + ".bias")), P(gc),
-             P(store.stat_acc(bn, "bwd")), xc.numel() // bn.c, bn.c, stream_ptr())
+             P(store.stat_acc(bn, "bwd", xc.numel() // bn.c)), xc.numel() // bn.c, bn.c, stream_ptr())
         return gc
 
     def _epi(self, store: Store, bn: BNSpec, xc, stats, y=None, bn2: Optional[BNSpec] = None, xc2=None, stats2=None,
-             skip00: bool = False) -> DgradBnEpi:
+             skip00: bool = False, append: bool = False) -> DgradBnEpi:
+        """append: this dgrad's partial sums follow those of the skip00 dgrad before it (a strided block's
+        downsample dgrad finishing the same BN reductions, include/avt.h)."""
         e = DgradBnEpi()
+        rows = xc.numel() // bn.c
         e.xc, e.y, e.stats = xc.data_ptr(), (y.data_ptr() if y is not None else None), stats.data_ptr()
-        e.acc = store.stat_acc(bn, "bwd").data_ptr()
+        e.acc = store.stat_acc(bn, "bwd", rows).data_ptr()
         if bn2 is not None:
-            e.xc2, e.stats2, e.acc2 = xc2.data_ptr(), stats2.data_ptr(), store.stat_acc(bn2, "bwd").data_ptr()
+            e.xc2, e.stats2, e.acc2 = xc2.data_ptr(), stats2.data_ptr(), store.stat_acc(bn2, "bwd", rows).data_ptr()
         e.skip_class00 = int(skip00)
+        e.append_slots = int(append)
         return e
 
     def backward_blocks(self, tape: Dict, g: torch.Tensor, store: Store, lo: int, hi: int, premasked: bool = False):
@@ -506,9 +455,9 @@ class Trunk:
             if bi > 0 and FUSE_BN_BWD:  # the next block down: its bn2 (+ downsample BN) backward rides on this dgrad
                 pb, pt = self.blocks[bi - 1], tape["blocks"][bi - 1]
                 has_d = pb["down"] is not None
-                mk = lambda skip00: self._epi(store, pb["bn2"], pt["c2"], pt["s2"], y=pt["out"],
-                                              bn2=pb["bnd"] if has_d else None, xc2=pt["cd"] if has_d else None,
-                                              stats2=pt["sd"] if has_d else None, skip00=skip00)
+                mk = lambda skip00, append=False: self._epi(
+                    store, pb["bn2"], pt["c2"], pt["s2"], y=pt["out"], bn2=pb["bnd"] if has_d else None,
+                    xc2=pt["cd"] if has_d else None, stats2=pt["sd"] if has_d else None, skip00=skip00, append=append)
                 epi = mk(False)
             if identity and gres is None:
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store, add=g, epi=epi, add_mask=t["om"])
@@ -520,6 +469,8 @@ class Trunk:
                 strided = blk["conv1"].stride == 2
                 g_x = self._dgrad(g_c1, N, Hc, Wc, blk["conv1"], store,
                                   epi=mk(True) if (epi is not None and strided) else None)
+                if epi is not None and strided:  # the BN sums go after those of the conv1 dgrad just issued
+                    epi = mk(False, append=True)
                 g_x = self._dgrad(g_cd, N, Hc, Wc, blk["down"], store, add=g_x, inplace=True, epi=epi)
             g = g_x
             premasked = epi is not None
@@ -535,7 +486,7 @@ class Trunk:
         H1, W1 = tape["H1"], tape["W1"]
         c0, st0 = tape["c0"], tape["st0"]
         g_c0 = torch.empty_like(c0)
-        ws = store.stat_acc(self.bn1, "bwd")
+        ws = store.stat_acc(self.bn1, "bwd", c0.numel() // 64)
         call("avt_stem_maxpool_bn_relu_bwd", P(g), P(tape["idx"]), P(tape["carg"]), P(c0), P(st0[0]), P(st0[1]),
              P(st0[2]), P(st0[3]), P(store.param(self.bn1.prefix + ".weight")),
              P(store.grad(self.bn1.prefix + ".weight")), P(store.grad(self.bn1.prefix + ".bias")), P(g_c0), P(ws),

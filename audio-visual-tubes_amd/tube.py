@@ -108,7 +108,7 @@ class R3DTrunk:
         """Conv3d (+ BN statistics) -> (y [b*T, H', W', K] bf16, stats [4, K], H', W')."""
         Ho, Wo = conv_out(H, spec.k, spec.stride, spec.pad), conv_out(W, spec.k, spec.stride, spec.pad)
         y = torch.empty(b * T, Ho, Wo, spec.cout, device=x.device, dtype=torch.bfloat16)
-        acc = store.stat_acc(bn, "fwd") if training else None
+        acc = store.stat_acc(bn, "fwd", b * T * Ho * Wo) if training else None
         wf = store.packed3d(spec)
         ev = ConvProfiler.begin()
         if spec.stem:  # 7 temporal taps folded into the 32 input channels (tube.hip)
@@ -277,7 +277,7 @@ class TubeEngine(AVEngine):
         dA = None if dA is None else dA.contiguous().float()
         call("avt_hardway_bwd_ex", P(tape["v"]), P(tape["an"]), P(tape["inv"]), P(tape["A0"]), P(tape["save"]),
              P(dlogits), B, Pn, C, self.epsilon, self.epsilon2, self.tau, 1, 1, None, None, None, P(dA), None, None,
-             P(dA0), None, None, P(gan), 0, stream_ptr())
+             P(dA0), None, None, P(gan), 0, P(self.head_ws(B, C)), stream_ptr())
         if rep > 1:
             gan_a = torch.empty(Ba, C, **f32)
             call("avt_sum_rep_rows_f32", P(gan), P(gan_a), Ba, rep, C, stream_ptr())

@@ -77,11 +77,16 @@ long long avt_peak_mfma_flops(int shape, int blocks, int iters);
 int avt_copy16(void* dst, const void* src, size_t bytes, int blocks, void* stream);
 
 /* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
-/* y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
- * statistics are accumulated into bn_acc (fp64 [avt_bn_slots()][K][3] = avt_bn_acc_doubles(K), zero on
- * entry, consumed and re-zeroed by avt_bn_finalize; consumed by avt_bn_apply_fin, the caller re-zeroes).
+/* BatchNorm statistics (deterministic).  A BN's fp64 accumulator holds a small header and one slot of
+ * partial sums per row tile (or persistent block / reduce block) of the launch that accumulates it, each
+ * slot written by exactly one block with plain stores -- no atomics, nothing to zero between uses, any
+ * contents on entry.  The finalize sums the slots in slot order, so identical inputs give bitwise identical
+ * statistics, gradients and updates on every run (model.py:112-154's CPU path is deterministic too).
+ * Forward: avt_bn_acc_doubles(rows, C) doubles; backward: avt_bn_bwd_workspace(rows, C) bytes.
+ *
+ * y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
+ * statistics are stored into bn_acc (avt_bn_acc_doubles(N*P*Q, K) doubles), for avt_bn_finalize.
  * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
-int avt_bn_slots(void);
 /* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
@@ -124,7 +129,8 @@ int avt_set_small_tiles(int waves);
 /* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
  * at least min_ktiles 32-pixel tiles per block */
 int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
-/* wgrad split-K partials go through a slab + reduce up to max_splits splits (fp32 atomics beyond);
+/* wgrad split-K partials go through a slab + reduce up to max_splits splits (default: all -- deterministic;
+ * beyond it fp32 atomics, whose summation order varies run to run; an A/B knob);
  * wave_cost = per-block fixed cost in k-tiles used by the wave model */
 int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 /* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
@@ -137,7 +143,7 @@ int avt_set_stem_kernel(int on);
 /* 1 (default, env AVT_STEM_WGRAD): the 7x7/s2 stem wgrads (C 4 or 1, K 64) run on the per-wave
  * LDS-patch kernel (needs the avt_conv2d_wgrad_workspace() slab; deterministic); 0: the generic one */
 int avt_set_stem_wgrad(int on);
-size_t avt_bn_acc_doubles(int C);
+size_t avt_bn_acc_doubles(long long rows, int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);
 /* dx[N,H,W,C] = dgrad(dy[N,P,Q,K], wt[C][R*S*K]) (+ add[N,H,W,C] if add != NULL; add may alias dx) */
@@ -172,10 +178,12 @@ int avt_conv2d_dgrad_ws(const void* dy, const void* wt, void* dx, const void* ad
 /* avt_conv2d_dgrad with the backward of the BatchNorm (+ReLU) that produced dx's positions fused into
  * its store epilogue (BasicBlock.forward, base_models.py:46-49, 58-67): the result g (after `add`) is
  * masked, g' = g * [y > 0] (y given: the block output) or g * [fma(xc, scale, shift) > 0] (y NULL:
- * BasicBlock.bn1's ReLU), dx = g' is stored, and sum g', sum g' * (xc - mean) * invstd are added into
- * acc (the avt_bn_bwd workspace layout, [avt_bn_slots()][C][2] fp64); xc2/stats2/acc2 (optional) a
- * second BN fed by the same g' (a first block's downsample.1).  skip_class00: for a stride-2 dgrad,
- * the (even, even) pixels are stored plain (a later in-place downsample dgrad finishes them). */
+ * BasicBlock.bn1's ReLU), dx = g' is stored, and sum g', sum g' * (xc - mean) * invstd are stored into
+ * acc (an avt_bn_bwd_workspace(N*H*W, C) workspace); xc2/stats2/acc2 (optional) a second BN fed by the
+ * same g' (a first block's downsample.1).  skip_class00: for a stride-2 dgrad, the (even, even) pixels are
+ * stored plain (a later in-place downsample dgrad finishes them).  append_slots: this call's partial sums
+ * go after those of the call before it on acc (that skip_class00 call: the downsample dgrad finishing the
+ * same BN's reduction); 0: this call's sums replace whatever acc held. */
 typedef struct {
   const void* xc;      /* [N,H,W,C] bf16 pre-BN activations */
   const void* y;       /* [N,H,W,C] bf16 ReLU output, or NULL */
@@ -185,6 +193,7 @@ typedef struct {
   const float* stats2;
   double* acc2;
   int skip_class00;
+  int append_slots;
 } avt_dgrad_bn_epi;
 int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* add, int N, int H, int W, int C, int K,
                         int R, int S, int stride, int pad, const avt_dgrad_bn_epi* epi, void* stream);
@@ -213,7 +222,7 @@ int avt_sum_rep_rows_f32(const float* in, float* out, int B, int rep, int C, voi
 
 /* ---- batch norm (train mode) ---- */
 /* merge bn_acc (see avt_conv2d_fwd) over `rows` rows -> scale, shift, mean, invstd (fp32 [C]);
- * running stats updated if non-NULL (momentum, unbiased var); bn_acc re-zeroed */
+ * running stats updated if non-NULL (momentum, unbiased var); bn_acc is read, not modified */
 int avt_bn_finalize(double* acc, long long rows, int C, const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, float* scale, float* shift, float* save_mean,
                     float* save_invstd, void* stream);
@@ -225,29 +234,11 @@ int avt_bn_finalize_rep(double* acc, long long rows, long long rep, int C, const
 /* out = [relu](x*scale+shift + [residual*rscale+rshift | residual]) over rows x C (NHWC rows) */
 int avt_bn_apply(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                  const float* rshift, void* out, long long rows, int C, int relu, void* stream);
-/* One train-mode BatchNorm's statistics for avt_bn_apply_fin */
-typedef struct {
-  double* acc;          /* avt_bn_acc_doubles(C) doubles from a conv epilogue (read, NOT re-zeroed) */
-  const float* gamma;   /* [C] */
-  const float* beta;
-  float* running_mean;  /* [C] updated (momentum, unbiased var) if non-NULL */
-  float* running_var;
-  float* stats;         /* out [4][C]: scale, shift, mean, invstd (as avt_bn_finalize) */
-} avt_bn_stat;
-/* avt_bn_finalize (of bn, and of bn_res when non-NULL) + avt_bn_apply[_mask] in one launch:
- * out = [relu](x*scale+shift + [residual*rscale+rshift | residual]), mask (optional, needs relu) as
- * avt_bn_apply_mask; scale/shift bitwise equal to avt_bn_finalize's.  rows: accumulated rows (each
- * standing for `rep` rows of the logical batch, see avt_bn_finalize_rep); C % 64 == 0.  Unlike
- * avt_bn_finalize it leaves the accumulators as they are: zero them before the next conv accumulates.  The forward of
- * BasicBlock.bn1+relu and of bn2 (+downsample.1) + residual + relu (base_models.py:46-49, 58-67). */
-int avt_bn_apply_fin(const void* x, const avt_bn_stat* bn, const void* residual, const avt_bn_stat* bn_res, void* out,
-                     void* mask, long long rows, long long rep, int C, int relu, float momentum, float eps,
-                     void* stream);
 /* avt_bn_apply with relu, also writing the ReLU mask of out as bits: mask [rows][C/8] u8, bit e of byte
  * j = out[.][8j+e] > 0 (the stored bf16 value) -- what the backward's relu mask reads instead of out */
 int avt_bn_apply_mask(const void* x, const float* scale, const float* shift, const void* residual, const float* rscale,
                       const float* rshift, void* out, void* mask, long long rows, int C, void* stream);
-/* bytes of bn_bwd workspace: its first avt_bn_slots()*C*2 doubles must be zero on entry (left zero) */
+/* bytes of the BN-backward workspace for up to `rows` rows (any contents on entry) */
 size_t avt_bn_bwd_workspace(long long rows, int C);
 /* g' = g*[y>0] (y may be NULL: no mask); dgamma += sum g'*xhat; dbeta += sum g';
  * gc = gamma*invstd*(g' - mean(g') - xhat*mean(g'*xhat)); gmask_out (optional) = g' */
@@ -263,7 +254,7 @@ typedef struct {
   float* dgamma;          /* [C] accumulated (+=), may be NULL */
   float* dbeta;
   void* gc;               /* [rows][C] bf16 output: gradient of xc */
-  void* workspace;        /* avt_bn_bwd_workspace(rows, C) bytes, accumulator zero on entry (left zero) */
+  void* workspace;        /* avt_bn_bwd_workspace(rows, C) bytes (any contents on entry) */
 } avt_bn_bwd_target;
 /* BasicBlock output backward (base_models.py:64-67): g' = g * mask (bits of avt_bn_apply_mask), then the
  * BN backward of t1 and -- if t2 != NULL -- of t2 (a first block's bn2 and downsample.1, which share g'),
@@ -316,7 +307,11 @@ int avt_hardway_bwd_ex(const void* v, const float* an, const float* inv, const f
                        const float* dlogits, int B, int P, int C, float eps1, float eps2, float tau, int trimap,
                        int use_neg, const float* dwA, const float* vsum, float* dm, const float* gA, const float* gPos,
                        const float* gNeg, float* dA0, float* dvh, void* gv, float* gan, int gan_accumulate,
-                       void* stream);
+                       float* ws, void* stream);
+/* ws (avt_hardway_bwd_ex / avt_hardway_attention_bwd): avt_hardway_bwd_ws_floats(B, C) floats for the split-K
+ * partials of the audio-vector gradient, summed in split order (deterministic); NULL: one split (slow).
+ * avt_hardway_bwd runs without it. */
+size_t avt_hardway_bwd_ws_floats(int B, int C);
 /* Standalone HardWayAttention()(audio_features, video_features) -> (A, logits) (model.py:38-60): fp32
  * features taken as given (the module does not normalise them; FullModel normalises before the call,
  * model.py:31-35), tri-map and Neg on.  v [B][P][C] fp32 = '(b t) (h w) c' of video_features,
@@ -329,7 +324,7 @@ int avt_hardway_attention_fwd(const float* v, const float* an, int B, int P, int
  * '(b t) (h w) c'), gan [B][C] fp32 (d audio features).  dA0 [B][P][B], dvh [B][P][C] fp32: workspace. */
 int avt_hardway_attention_bwd(const float* v, const float* an, const float* inv, const float* A0, const float* save,
                               const float* dlogits, const float* gA, int B, int P, int C, float eps1, float eps2,
-                              float tau, float* dA0, float* dvh, float* gv, float* gan, void* stream);
+                              float tau, float* dA0, float* dvh, float* gv, float* gan, float* ws, void* stream);
 /* train_hardway.py:134-142 loss combination of the 16-frame two-view step: given the two CE values
  * (avt_hardway_ce outputs; their dlogits use scale loss_weight/2) and weighted_A of both views
  * ([b*t][P], '(b t)' clip-major), out[5] = {combined, hardway, aug, l2, consistency} and

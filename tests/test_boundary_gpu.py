@@ -90,7 +90,8 @@ def test_head_grads_through_A_Pos_Neg(B, trimap):
     dA0, dvh, gv, gan = torch.empty(B, Pn, B, **f32), torch.empty(B, Pn, C, **f32), torch.empty_like(vd), \
         torch.empty(B, C, **f32)
     call("avt_hardway_bwd_ex", P(vd), P(ad), P(inv), P(A0), P(save), P(dl), B, Pn, C, 0.65, 0.4, 0.03, int(trimap), 1,
-         None, None, None, P(rA.to(DEV)), P(rP.to(DEV)), P(rN.to(DEV)), P(dA0), P(dvh), P(gv), P(gan), 0, S())
+         None, None, None, P(rA.to(DEV)), P(rP.to(DEV)), P(rN.to(DEV)), P(dA0), P(dvh), P(gv), P(gan), 0,
+         P(torch.empty(int(query("avt_hardway_bwd_ws_floats", B, C)), **f32)), S())
     torch.cuda.synchronize()
     vt = v.double().permute(0, 3, 1, 2).requires_grad_(True)
     at = an.double().requires_grad_(True)
@@ -272,7 +273,7 @@ def test_lr_change_after_capture_reaches_replays():
     d = (m_g._flat.flat - before).abs().max().item()
     assert 1e-6 < d <= 3e-6 * 1.05 + 1e-7, d
     diff = (m_g._flat.flat - m_e._flat.flat).abs().max().item()
-    assert diff <= 1.1e-5, diff  # <= lr per step; split-K / BN atomics can flip a ~0 gradient's update
+    assert diff == 0.0, diff  # graph replays and eager steps: the same deterministic kernels, the same bits
 
 
 def test_short_last_batch_after_capture_runs_eagerly():

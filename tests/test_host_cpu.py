@@ -33,9 +33,10 @@ def test_library_exports_every_declared_symbol():
         assert s in _lib.SIGNATURES, f"{s} declared in avt.h but not bound in _lib.SIGNATURES"
     assert lib.avt_abi_version() == 1
     # pure host queries need no GPU
-    slots = _lib.query("avt_bn_slots")
-    assert slots % 16 == 0  # the finalize kernels spread the slots over 16 lanes
-    assert _lib.query("avt_bn_acc_doubles", 64) == slots * 64 * 3
+    # BN accumulators: 8-double header + one slot per 64 rows (+ 520 for persistent / reduce grids)
+    assert _lib.query("avt_bn_acc_doubles", 6400, 64) == 8 + (100 + 520) * 64 * 3
+    assert _lib.query("avt_bn_bwd_workspace", 6400, 64) == (8 + 64 + (100 + 520) * 64 * 2) * 8
+    assert _lib.query("avt_hardway_bwd_ws_floats", 128, 512) == 64 * 128 * 512
     assert _lib.query("avt_pack_desc_bytes") == 48
     assert _lib.query("avt_hardway_save_floats", 8) == 8 * 20
 

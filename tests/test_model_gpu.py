@@ -198,3 +198,26 @@ def test_eval_mode_uses_running_stats(golden_dir):
     rA, rlog, _, _, _ = orc.avenet_forward(sd, img.double(), aud.double(), None, training=False)
     assert (A.cpu().double() - rA).abs().max() < 3e-2
     assert int(model.state_dict()["imgnet.bn1.num_batches_tracked"]) == 0
+
+
+def test_train_step_is_deterministic():
+    """two runs of the fused train step from the same weights on the same inputs give
+    bitwise-equal losses, gradients, weights and BN running statistics -- no atomics in any reduction
+    (BN statistics in ordered slots, wgrad split-K through slabs, the head's split-K summed in split order),
+    so neither the arrival order of blocks nor the two-stream schedule changes a bit."""
+    from avt_amd.model import AVENet, HardWayArgs
+    from avt_amd.train import HardWayTrainStep
+
+    img, aud = orc.make_image(6, 96), orc.make_spectrogram(6, 97, 110)
+    runs = []
+    for _ in range(2):
+        m = AVENet(HardWayArgs(), False)
+        m.load_state_dict(orc.make_state(3))
+        m = m.to(DEV).train()
+        step = HardWayTrainStep(m, lr=1e-4, weight_decay=1e-4)
+        losses = [step.step(img.to(DEV), aud.to(DEV)).item() for _ in range(3)]
+        torch.cuda.synchronize()
+        runs.append((losses, step.grad.clone(), m._flat.flat.clone(), m._flat.bflat.clone()))
+    (l0, g0, w0, b0), (l1, g1, w1, b1) = runs
+    assert l0 == l1
+    assert torch.equal(g0, g1) and torch.equal(w0, w1) and torch.equal(b0, b1)

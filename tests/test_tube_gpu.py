@@ -69,7 +69,8 @@ def test_conv3d_fwd_and_bn_stats(case):
     call("avt_pack_conv3d_weight", P(wd), P(wp), K, C, 3, 3, 3, 0, S())
     Ho, Wo = (H + 2 - 3) // st + 1, (W + 2 - 3) // st + 1
     y = torch.empty(N, T, Ho, Wo, K, device=DEV, dtype=torch.bfloat16)
-    acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=DEV, dtype=torch.float64)
+    acc = torch.full((int(query("avt_bn_acc_doubles", N * T * Ho * Wo, K)),), float("nan"), device=DEV,
+                     dtype=torch.float64)
     xd = x.to(DEV)
     call("avt_conv3d_fwd", P(xd), P(wp), P(y), P(acc), N, T, H, W, C, K, 3, 3, 3, st, 1, 1, S())
     ref = F.conv3d(x.double().permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).double(), stride=(1, st, st), padding=1)

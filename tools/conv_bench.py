@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
     ap.add_argument("--only", default="")
     ap.add_argument("--wgrad-policy", default="0,4", help="';'-separated target_blocks,min_kt (0 = wave model)")
-    ap.add_argument("--slab-max", default="32,16", help="avt_set_wgrad_slab_max(max_splits, wave_cost)")
+    ap.add_argument("--slab-max", default="1073741824,16", help="avt_set_wgrad_slab_max(max_splits, wave_cost)")
     ap.add_argument("--wgrad-tiles", default="1", help="comma list of avt_set_wgrad_tiles values to sweep")
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
@@ -90,7 +90,7 @@ def main():
         y = torch.empty(N, Pq, Qq, K, device=dev, dtype=torch.bfloat16)
         dx = torch.empty(N, H, W, C, device=dev, dtype=torch.bfloat16)
         dw = torch.zeros(K, R, R, C, device=dev)
-        acc = torch.zeros(16 * K * 3, device=dev, dtype=torch.float64)
+        acc = torch.empty(int(query("avt_bn_acc_doubles", N * Pq * Qq, K)), device=dev, dtype=torch.float64)
         flops = 2.0 * N * Pq * Qq * K * C * R * R
         line = f"{name:12s} M={N * Pq * Qq:7d} N={K:4d} K={kg:5d}"
         if args.halo and R == 3 and st == 1:

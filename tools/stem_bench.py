@@ -52,7 +52,7 @@ def main():
         wf = torch.empty(K, kg, device=dev, dtype=torch.bfloat16)
         call("avt_pack_conv_weight", P(w), K, R, R, cin, cp, kg, P(wf), None, S())
         y = torch.empty(N, OH, OW, K, device=dev, dtype=torch.bfloat16)
-        acc = torch.zeros(int(query("avt_bn_acc_doubles", K)), device=dev, dtype=torch.float64)
+        acc = torch.empty(int(query("avt_bn_acc_doubles", N * OH * OW, K)), device=dev, dtype=torch.float64)
         flops = 2.0 * N * OH * OW * K * R * R * cin
         out_bytes = 2.0 * N * OH * OW * K
         line = f"{name:7s} N={N}"
