@@ -19,8 +19,7 @@
  *   avt_bn_apply_mask,           BasicBlock output relu(bn2(c2) + residual) (base_models.py:64-67) with its ReLU
  *   avt_bn_bwd_mask,             mask kept as bits; the backward of bn2 (+ downsample.1) from those bits, and the
  *   avt_conv2d_dgrad_mask        identity block's input gradient dgrad(conv1) + g * mask without a stored g'
- *   avt_set_c64 / avt_set_halo   A/B knobs of the layer-1 resident-weight and halo-reuse conv kernels
- *   avt_set_s2_dgrad_one         A/B knob: the stride-2 dgrad's four parity classes in one launch
+ *   (avt_set_*: A/B knobs between measured kernel variants, in avt_tuning.h -- not part of this boundary)
  *   avt_audio_pool_norm_fwd/bwd  nn.AdaptiveMaxPool2d((1,1)) + F.normalize(dim=1) (model.py:96, 120-122)
  *   avt_hardway_fwd/bwd          AVENet.forward head: normalize, A/A0 einsums, sigmoid trimap,
  *                                sim1/sim/sim2, logits/0.07, weighted_A (model.py:114-154);
@@ -87,62 +86,6 @@ int avt_copy16(void* dst, const void* src, size_t bytes, int blocks, void* strea
  * y[N,P,Q,K] = conv(x[N,H,W,Cp], wpack[K][Kg]); if bn_acc != NULL the fp32 results' batch-norm
  * statistics are stored into bn_acc (avt_bn_acc_doubles(N*P*Q, K) doubles), for avt_bn_finalize.
  * Cp is 1 or 4 (stems, Kg = R*S*Cp rounded up to 32) or a multiple of 32 (Kg = R*S*Cp). */
-/* conv kernel family for fwd/dgrad: 1 = LDS-DMA pipelined (default), 0 = register-staged
- * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
-int avt_set_conv_variant(int variant);
-/* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) and nst64 (64 x 128
- * small-batch tile) in 2..5 (3 or more: one block per CU); all settings give bitwise-identical results (A/B knob) */
-int avt_set_halo_stages(int nst128, int nst64);
-/* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
- * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
- * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
- * — an A/B knob */
-int avt_set_nt64_config(int cfg);
-/* 1 (default; env AVT_HALO): 3x3 stride-1 fwd/dgrad with C % 64 == 0 and K % 128 == 0 run on the halo-reuse
- * kernel (each input pixel moved to LDS once per 64-channel chunk instead of once per tap): 4-wave 128x128
- * tiles for W <= 19 (layer3/4), 8-wave 256x128 tiles for W <= 79 (layer2); 0: tap-gather kernel everywhere;
- * 2: the 8-wave forms for every width (and 256x64 for K = 64) — an A/B knob */
-int avt_set_halo(int on);
-/* 1 (default; env AVT_HALO8): under avt_set_halo(1), layer3/4 shapes also take the 8-wave 256x128 halo
- * tile where it measured faster (C >= 512, or 256-row tiles fitting one wave of blocks); 0: the 4-wave
- * 128x128 tile for every W <= 19 shape; -1: back to the environment default — an A/B knob */
-int avt_set_halo8(int on);
-/* 1: the halo fwd/dgrad tiles run on v_mfma_f32_16x16x32_bf16 (2x2 per 32x32 block) instead of 32x32x16;
- * 0: 32x32x16; -1: the environment default (AVT_HALO_MF16) — an A/B knob (fp32 sums in another order) */
-int avt_set_halo_mf16(int on);
-/* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
- * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
- * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */
-int avt_set_c64(int on);
-/* 1 (default; env AVT_S2_ONE): a stride-2 dgrad without the BN-backward epilogue runs its output parity
- * classes (each with only the taps that reach it) as ONE launch, blocks of the classes with the most taps
- * dispatched first; 0: one launch per class.  The results are bitwise identical (same tap order). */
-int avt_set_s2_dgrad_one(int on);
-/* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
- * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
- * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */
-int avt_set_nt128_config(int cfg);
-/* fwd/dgrad tiles of 64 rows (64x128 / 64x64; a 64x128 halo tile for layer3/4) when the 128-row tile
- * grid would give fewer than `waves` blocks per CU (small per-GPU batches); 0 = never, -1 = always;
- * default 1 (env AVT_SMALL_TILES) */
-int avt_set_small_tiles(int waves);
-/* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
- * at least min_ktiles 32-pixel tiles per block */
-int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
-/* wgrad split-K partials go through a slab + reduce up to max_splits splits (default: all -- deterministic;
- * beyond it fp32 atomics, whose summation order varies run to run; an A/B knob);
- * wave_cost = per-block fixed cost in k-tiles used by the wave model */
-int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
-/* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
-int avt_set_wgrad_tiles(int big);
-/* 3x3/s1 wgrads on the halo-reuse kernel (1; env AVT_WGRAD_HALO) or the tap-gather one (0, default) */
-int avt_set_wgrad_halo(int on);
-/* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
- * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */
-int avt_set_stem_kernel(int on);
-/* 1 (default, env AVT_STEM_WGRAD): the 7x7/s2 stem wgrads (C 4 or 1, K 64) run on the per-wave
- * LDS-patch kernel (needs the avt_conv2d_wgrad_workspace() slab; deterministic); 0: the generic one */
-int avt_set_stem_wgrad(int on);
 size_t avt_bn_acc_doubles(long long rows, int C);
 int avt_conv2d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
                    int R, int S, int stride, int pad, int Kg, void* stream);
@@ -163,10 +106,6 @@ int avt_conv2d_dgrad_mask(const void* dy, const void* wt, void* dx, const void* 
  * 0 plans it as the smallest divisor whose grid reaches `blocks` (0: two per CU). */
 int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, int S, int stride, int pad, int dgrad,
                            long long* part_floats, int* counters);
-int avt_set_halo_splitk(int ksplit, int target_blocks);
-/* TN wgrad LDS ring depth: nst for the 4-wave tiles (4 default, 6, 8), nst_big for the 8-wave 256 x 256
- * tile (3 default, 4, 5) -- deeper rings keep more k-tiles in flight for a block alone on its CU */
-int avt_set_wgrad_nst(int nst, int nst_big);
 /* part_floats / counters: the sizes of part and cnt as allocated; the plan is re-made at every call from the
  * current knobs, and a call whose plan needs more than the workspace holds runs without split-K. */
 int avt_conv2d_fwd_ws(const void* x, const void* wpack, void* y, double* bn_acc, int N, int H, int W, int Cp, int K,
@@ -395,6 +334,8 @@ int avt_nchw_to_nhwc_bf16(const float* x, void* y, int N, int C, int H, int W, i
  * train_hardway.py:130-131 fused with the NHWC/bf16 conversion */
 int avt_ncthw_to_nhwc_bf16(const float* x, void* y, int N, int C, int T, int H, int W, int Cp, void* stream);
 int avt_nhwc_bf16_to_nchw(const void* x, float* y, int N, int C, int HW, void* stream);
+
+#include "avt_tuning.h"  /* A/B knobs (process-global; not part of the drop-in path) */
 
 #ifdef __cplusplus
 }

@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _header_symbols():
-    txt = open(os.path.join(REPO, "include", "avt.h")).read()
+    txt = "".join(open(os.path.join(REPO, "include", h)).read() for h in ("avt.h", "avt_tuning.h"))
     return sorted(set(re.findall(r"\b(avt_[a-z0-9_]+)\s*\(", txt)))
 
 
