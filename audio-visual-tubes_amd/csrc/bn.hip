@@ -570,48 +570,57 @@ __global__ __launch_bounds__(256) void stem_bn_relu_maxpool_fwd_kernel(
 // LDS capacity for the two pooled rows a bwd block reads: 2 x Q x C x (2 B grad + 1 B argmax)
 constexpr int kStemLdsBytes = 48 * 1024;
 
-__global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
+// One block per PAIR of input rows (2p, 2p+1) of image n: the windows covering them are pooled rows p
+// (row 2p: window row kh = 1; row 2p+1: kh = 2) and p+1 (row 2p+1: kh = 0), so the block stages those two
+// pooled rows of gy and argmax into LDS once for both input rows (a row per block staged ~1.5 pooled rows
+// per input row) and has twice the items in flight.  For input pixel (h, w) the candidate windows are
+// (p_h, q) with q = w/2 (kw = 1 if w even, 2 if odd) and, for odd w, q+1 (kw = 0); g' = [h0 > 0] * the
+// sum of gy over the candidates whose argmax is (h, w); gc = gamma*invstd*(g' - k1 - xhat*k2).
+constexpr int kStemBwdThreads = 512;
+__global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_kernel(
     const bf16_t* __restrict__ gy, const unsigned char* __restrict__ idx, const bf16_t* __restrict__ c,
     const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ k1,
     const float* __restrict__ k2, bf16_t* __restrict__ gc, int H, int W, int C, int cvs, int P, int Q) {
   extern __shared__ __attribute__((aligned(16))) char lds[];  // 6*Q*C bytes (dynamic)
-  const int row = blockIdx.x;  // n * H + h
-  const int n = row / H, h = row - n * H;
+  const int hp = (H + 1) >> 1;
+  const int n = blockIdx.x / hp, p = blockIdx.x - n * hp;
   const int cv = 1 << cvs;
-  // Windows covering input row h: p0 = h/2 (window row kh = 1 if h even, 2 if odd) and, for odd
-  // h, p0 + 1 (kh = 0); likewise for columns.  The block first stages those (<= 2) pooled rows of
-  // gy and argmax into LDS with coalesced 16-B copies, so each pooled element is fetched from
-  // memory once per block instead of once per covering input pixel.
-  const int p0 = h >> 1, kh0 = h - 2 * p0 + 1;
-  const bool p_two = (h & 1) && p0 + 1 < P;
-  const int np = p_two ? 2 : 1;
+  const bool two_rows = 2 * p + 1 < H;
+  const bool p_next = p + 1 < P;
   const int rowg = Q * C * 2, rowi = Q * C;  // bytes of one pooled row of gy / argmax
   bf16_t* lg = reinterpret_cast<bf16_t*>(lds);
   unsigned char* li = reinterpret_cast<unsigned char*>(lds + 2 * rowg);
-  // the pre-activations of this thread's (<= kStemItems) items are loaded first: they do not depend on
-  // the staged rows, so their HBM latency overlaps the staging and its barrier
-  constexpr int kStemItems = 6;
-  u32x4 cx[kStemItems];
+  const int items_row = W * cv, items = (two_rows ? 2 : 1) * items_row;
+  // the pre-activations of this thread's items first: independent of the staged rows, their HBM latency
+  // overlaps the staging and its barrier
+  constexpr int kItems = 6;
+  u32x4 cx[kItems];
+  const size_t img_row0 = (size_t)n * H + 2 * p;  // input row 2p of image n
 #pragma unroll
-  for (int j = 0; j < kStemItems; ++j) {
-    const int t = threadIdx.x + 256 * j;
-    if (t < W * cv) cx[j] = *reinterpret_cast<const u32x4*>(c + ((size_t)row * W) * C + (size_t)t * 8);
+  for (int j = 0; j < kItems; ++j) {
+    const int t = threadIdx.x + kStemBwdThreads * j;
+    if (t < items) cx[j] = *reinterpret_cast<const u32x4*>(c + (img_row0 * W) * C + (size_t)t * 8);
   }
-  for (int k = 0; k < np; ++k) {
-    const size_t prow = (size_t)n * P + p0 + k;
+  for (int k = 0; k < (p_next ? 2 : 1); ++k) {
+    const size_t prow = (size_t)n * P + p + k;
     const u32x4* sg = reinterpret_cast<const u32x4*>(gy + prow * Q * C);
     const u32x4* si = reinterpret_cast<const u32x4*>(idx + prow * Q * C);
-    for (int t = threadIdx.x; t < rowg / 16; t += 256) reinterpret_cast<u32x4*>(lg + k * Q * C)[t] = sg[t];
-    for (int t = threadIdx.x; t < rowi / 16; t += 256) reinterpret_cast<u32x4*>(li + k * rowi)[t] = si[t];
+    for (int t = threadIdx.x; t < rowg / 16; t += kStemBwdThreads) reinterpret_cast<u32x4*>(lg + k * Q * C)[t] = sg[t];
+    for (int t = threadIdx.x; t < rowi / 16; t += kStemBwdThreads) reinterpret_cast<u32x4*>(li + k * rowi)[t] = si[t];
   }
   __syncthreads();
-  const int k1r = p_two ? 1 : 0;  // LDS row of the second window row (aliases the first if none)
 #pragma unroll
-  for (int j = 0; j < kStemItems; ++j) {
-    const int t = threadIdx.x + 256 * j;
-    if (t >= W * cv) break;
-    const int w = t >> cvs, c8 = t & (cv - 1);
+  for (int j = 0; j < kItems; ++j) {
+    const int t = threadIdx.x + kStemBwdThreads * j;
+    if (t >= items) break;
+    const int r = t >= items_row ? 1 : 0;  // input row 2p + r
+    const int tw = t - r * items_row;
+    const int w = tw >> cvs, c8 = tw & (cv - 1);
+    // window row of (2p + r) in pooled row p: kh0 = 1 + r; in pooled row p + 1 (odd rows only): kh0 - 2
+    const int kh0 = 1 + r;
+    const bool p_two = r == 1 && p_next;
+    const int k1r = p_two ? 1 : 0;  // LDS row of the second window row (aliases the first if none)
     const int q0 = w >> 1, kw0 = w - 2 * q0 + 1;
     const bool q_two = (w & 1) && q0 + 1 < Q;
     const int q1 = q_two ? q0 + 1 : q0;
@@ -641,7 +650,7 @@ __global__ __launch_bounds__(256) void stem_maxpool_bn_bwd_apply_kernel(
       a += ((int)((i11 >> sh8) & 0xff) == pos11) ? f11[e] : 0.f;
       gg[e] = a;
     }
-    const size_t xo = ((size_t)row * W + w) * C + c8 * 8;
+    const size_t xo = ((img_row0 + r) * W + w) * C + c8 * 8;
     unpack8(cx[j], xx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -902,7 +911,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   AVT_REQUIRE(gy && idx && carg && c && scale && shift && mean && invstd && gamma && gc && workspace,
               "stem_maxpool_bn_relu_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "stem_maxpool_bn_relu_bwd: C=%d unsupported", C);
-  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)W * (C / 8) <= 6 * 256,
+  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)2 * W * (C / 8) <= 6 * kStemBwdThreads,
               "stem_maxpool_bn_relu_bwd: W=%d C=%d too wide", W, C);
   AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_maxpool_bn_relu_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");
@@ -915,7 +924,8 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
                        (long long)N * P * Q, C, st);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
-  hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * H), dim3(256), (size_t)6 * Q * C, st, (const bf16_t*)gy,
+  hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * ((H + 1) / 2)), dim3(kStemBwdThreads), (size_t)6 * Q * C,
+                     st, (const bf16_t*)gy,
                      (const unsigned char*)idx, (const bf16_t*)c, scale, shift, mean, invstd, gamma, k1, k2,
                      (bf16_t*)gc, H, W, C, ilog2(C / 8), P, Q);
   return check_launch("stem_maxpool_bn_relu_bwd");

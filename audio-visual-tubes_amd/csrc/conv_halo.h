@@ -69,8 +69,14 @@ constexpr int halo_blocks_per_cu() {
   return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
+// STAG (8-wave tiles, two waves per SIMD running the same program between per-tap barriers, which keeps them
+// in lockstep -- both SIMD partners reach their MFMAs, their LDS reads and the barrier together;
+// MI355X_MICROARCH.md "Two waves per SIMD" item 9): bit 0 = waves NW/2.. defer each tap step's last k-step
+// MFMAs past the next barrier (into the segment where their partners read fragments and issue DMA; the
+// fragments stay in registers, the accumulation order is unchanged: bitwise the same results); bit 1 = those
+// waves run at s_setprio 1 in the main loop (item 4)
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
-          bool MF16 = false>
+          bool MF16 = false, int STAG = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   static_assert(!(MF16 && SPLIT), "split-K runs the 32x32x16 form");
@@ -230,6 +236,21 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
   bf16x8 af[2][FM], bfr[2][FN];
+  auto mma = [&](int buf) {
+    if (HALO_DBG(8)) return;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (MF16)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
+      }
+  };
+  constexpr int LASTB = (KS - 1) & 1;  // fragment buffer of a step's last k-step
+  const bool late = (STAG & 1) && wid >= NW / 2;  // wave-uniform
+  if ((STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   for (int c = 0; c < nchunk; ++c) {
     const char* Ab = smem + (c & 1) * ABUF;  // patch buffer of this chunk
 #pragma unroll
@@ -271,28 +292,25 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
           const int stn = NSTB == 2 ? (stage ^ 1) : (stage + NSTB - 1) % NSTB;
           issue(cn, tn, stn);
         }
+        if (late && (t > 0 || c > 0)) {  // the previous step's deferred last k-step (its fragments in LASTB)
+          __builtin_amdgcn_sched_barrier(0);
+          mma(LASTB);
+          __builtin_amdgcn_sched_barrier(0);
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           if (ks + 1 < KS) {
             load_frags(ks + 1, (ks + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
           }
-          if (!HALO_DBG(8)) {
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-#pragma unroll
-              for (int j = 0; j < FN; ++j) {
-                if constexpr (MF16)
-                  acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
-                else
-                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
-              }
-          }
+          if (ks + 1 < KS || !late) mma(ks & 1);
           if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
   }
+  if (late) mma(LASTB);  // the last step's deferred k-step
+  if (STAG & 2) __builtin_amdgcn_s_setprio(0);
   wait_vmcnt<0>();
   __syncthreads();
 

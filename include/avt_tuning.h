@@ -37,6 +37,13 @@ int avt_set_halo8(int on);
 /* 1: the halo fwd/dgrad tiles run on v_mfma_f32_16x16x32_bf16 (2x2 per 32x32 block) instead of 32x32x16;
  * 0: 32x32x16; -1: the environment default (AVT_HALO_MF16) — an A/B knob (fp32 sums in another order) */
 int avt_set_halo_mf16(int on);
+/* the 8-wave halo tiles' SIMD-partner stagger: bit 0 = waves 4-7 run each tap step's last k-step of MFMAs
+ * after the next barrier (bitwise the same results), bit 1 = waves 4-7 at s_setprio 1 in the main loop;
+ * -1: the environment default (AVT_HALO_STAG, 0) — an A/B knob */
+int avt_set_halo_stagger(int mode);
+/* the same for the 8-wave TN wgrad blocks (the 256-wide layer4 tiles and the two-group 128 x 128 pairs);
+ * -1: the environment default (AVT_WGRAD_STAG, 0) — an A/B knob */
+int avt_set_wgrad_stagger(int mode);
 /* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
  * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */

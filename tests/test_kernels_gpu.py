@@ -1027,3 +1027,58 @@ def test_strided_dgrad_skip00_then_downsample_epilogue(case):
     tol = 1e-5 * gm.abs().sum((0, 1, 2)).max().item() + 1e-6
     np.testing.assert_allclose(a[:, 0].numpy(), s1.numpy(), atol=tol)
     np.testing.assert_allclose(a[:, 1].numpy(), s2.numpy(), atol=tol * 4)
+
+
+@pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (5, 14, 14, 512, 512, 3, 1, 1),
+                                  (2, 33, 38, 128, 128, 3, 1, 1), (1, 28, 28, 128, 128, 3, 1, 1)])
+def test_halo_stagger_bitwise_equal(case, mf16):
+    """The 8-wave halo tiles' SIMD-partner stagger (avt_set_halo_stagger: waves 4-7 run each tap step's last
+    k-step after the next barrier, and/or at s_setprio 1) moves MFMAs in time, not in accumulation order:
+    outputs, dgrads (plain and with the BN epilogue's mask) and BN partial sums are bitwise equal."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 61).relu().to(DEV)
+    g = torch.Generator().manual_seed(62)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, R * R * C)
+    dy = _rand_act(N, H, W, K, 63).to(DEV)
+    call("avt_set_halo8", 1)
+    outs = []
+    try:
+        for mode in (0, 1, 2, 3):
+            call("avt_set_halo_stagger", mode)
+            y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+            acc = fwd_acc(N * H * W, K)
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
+            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+            torch.cuda.synchronize()
+            outs.append((y.view(torch.int16).clone(), dx.view(torch.int16).clone(), acc_sums(acc, K, 3)))
+    finally:
+        call("avt_set_halo_stagger", -1)
+        call("avt_set_halo8", -1)
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+        assert torch.equal(o[2], outs[0][2])
+
+
+@pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (8, 14, 14, 256, 512, 3, 1, 1),
+                                  (2, 33, 38, 128, 128, 3, 1, 1), (4, 28, 28, 128, 128, 3, 1, 1)])
+def test_wgrad_stagger_bitwise_equal(case):
+    """The 8-wave TN wgrad blocks' stagger (avt_set_wgrad_stagger; the 256-wide layer4 tiles and the two-group
+    128 x 128 pairs) changes when MFMAs run, not the order they accumulate in: dw is bitwise equal, and the
+    deterministic slab reduce makes repeated runs bitwise equal too."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 71).relu().to(DEV)
+    dy = _rand_act(N, H, W, K, 72).to(DEV)
+    outs = []
+    try:
+        for mode in (0, 0, 1, 2, 3):
+            call("avt_set_wgrad_stagger", mode)
+            dw = torch.zeros(K, R, R, C, device=DEV)
+            wgrad(x, dy, dw, N, H, W, C, C, K, R, st, pad)
+            torch.cuda.synchronize()
+            outs.append(dw.clone())
+    finally:
+        call("avt_set_wgrad_stagger", -1)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
