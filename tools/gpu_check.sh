@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: the steps given as arguments, in order.  Every GPU step runs under its own time
 # limit; a failing step ends the session (no further GPU work after a crash, abort or timeout).
-#   tests                  full GPU parity suite, then smoke()
+#   tests                  full GPU parity suite (stops at the first failure; MAXFAIL=n for more), then smoke()
 #   t:<pytest args>        a subset of the GPU tests, e.g. "t:tests/test_kernels_gpu.py -k 'halo or c64'" (eval'd)
 #   bench:<tag>:<args>     python bench.py <args>  -> gpurun_out/bench_<tag>.log (last line = the JSON)
 #   prof:<tag>:<args>      rocprofv3 --kernel-trace --stats over bench.py --steps 5 --warmup 2 <args>
@@ -17,7 +17,7 @@ for step in "$@"; do
   kind=${step%%:*}; rest=${step#*:}
   case "$kind" in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider \
+      timeout -k 10 900 python -u -m pytest tests --maxfail=${MAXFAIL:-1} -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider \
         > gpurun_out/gpu_tests.log 2>&1; rc=$?
       echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" gpurun_out/gpu_tests.log | tail -8
       [ $rc -ne 0 ] && exit $rc
