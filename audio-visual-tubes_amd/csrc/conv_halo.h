@@ -258,24 +258,29 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       {
         // step s = c*9 + t: its stage is s % NSTB -- (c + t) % 2 for NSTB 2 (9 odd), t % 3 for 3
         const int stage = NSTB == 2 ? (c + t) & 1 : NSTB == 3 ? t % 3 : (c * 9 + t) % NSTB;
-        // step s has landed once only steps s+1 .. s+NSTB-2 may be outstanding (issued after it): BR weight
-        // loads each, + AP patch loads for those with a tap >= NSTB-1 (t is a constant after unrolling)
-        if constexpr (NSTB == 2) {
-          wait_vmcnt<0>();
-        } else {
-          int pieces = 0;
+        // step s's weight tile has landed once only what was issued after it may be outstanding: step s's own
+        // patch piece (issued right after its weights; a piece of the NEXT chunk, read only from that chunk's
+        // first step, whose wait -- tap 0 carries no piece -- covers every piece issued before it) and steps
+        // s+1 .. s+NSTB-2: BR weight loads each + AP for those with a tap >= NSTB-1 (t is a constant after
+        // unrolling).  Leaving the own piece outstanding gives every piece one more step to land (the patch
+        // is the operand that misses L2).  -DAVT_HALO_STRICT_WAIT: the step's own piece is waited for too.
+        int pieces = 0;
+#ifndef AVT_HALO_STRICT_WAIT
+        pieces += (t >= NSTB - 1) ? 1 : 0;
+#endif
 #pragma unroll
-          for (int j = 1; j <= NSTB - 2; ++j) pieces += ((t + j) % 9 >= NSTB - 1) ? 1 : 0;
-          constexpr int W0 = (NSTB - 2) * BR;
-          if (pieces == 0)
-            wait_vmcnt<W0>();
-          else if (pieces == 1)
-            wait_vmcnt<W0 + AP>();
-          else if (pieces == 2)
-            wait_vmcnt<W0 + 2 * AP>();
-          else
-            wait_vmcnt<W0 + 3 * AP>();
-        }
+        for (int j = 1; j <= NSTB - 2; ++j) pieces += ((t + j) % 9 >= NSTB - 1) ? 1 : 0;
+        constexpr int W0 = (NSTB - 2) * BR;
+        if (pieces == 0)
+          wait_vmcnt<W0>();
+        else if (pieces == 1)
+          wait_vmcnt<W0 + AP>();
+        else if (pieces == 2)
+          wait_vmcnt<W0 + 2 * AP>();
+        else if (pieces == 3)
+          wait_vmcnt<W0 + 3 * AP>();
+        else
+          wait_vmcnt<W0 + 4 * AP>();
         if (!HALO_DBG(4)) __builtin_amdgcn_s_barrier();
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
         auto load_frags = [&](int ks, int buf) {
