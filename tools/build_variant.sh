@@ -3,6 +3,7 @@
 # A/B runs (AVT_LIB_PATH=...).  usage: bash tools/build_variant.sh libavt_base.so -DAVT_BN_SLOTS=16
 set -e
 NAME=$1; shift
+[ "$NAME" = libavt.so ] && { echo "build libavt.so with __graft_entry__.build() (it records the source hash)"; exit 2; }
 R=$(cd "$(dirname "$0")/.." && pwd)
 W=$(mktemp -d /tmp/avt_var_XXXX)
 objs=""
