@@ -35,51 +35,58 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// 16 lanes per channel, lane s owning slots s, s+16, s+32, ... in four interleaved partial sums (slots
-// s + 16(4i+q) into partial q, then (p0+p1)+(p2+p3)): independent loads in flight, a fixed summation
-// order; the lanes' sums meet by shuffles in a fixed tree.  Launch: 16 channels per 256-thread block.
-__device__ __forceinline__ double sum16(double v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 16);
-  return v;
-}
-// lane s's shares of the W elements of channel c over the slots of accumulator acc (header + slots)
+// The slot sums of 16 consecutive channels [c0, c0 + 16), W statistics each, in a fixed order: wave w of the
+// block adds slots w, w + kFinWaves, w + 2 kFinWaves, ... in turn (16 independent loads in flight per
+// batch); lane l < 16 W owns element l = (channel c0 + l / W, statistic l % W) of a slot's 16-channel run, so a
+// slot is one coalesced 8 B/lane load.  The waves' partials meet in LDS in wave order; tot[l] on return
+// (after a barrier).  Launch: kFinThreads threads per 16 channels.
+constexpr int kFinWaves = 16, kFinThreads = kFinWaves * 64;
 template <int W>
-__device__ __forceinline__ void lane_slots(const double* __restrict__ acc, const double* __restrict__ slots, int C,
-                                           int c, int s, double* out) {
+__device__ __forceinline__ void slot_sums16(const double* __restrict__ acc, const double* __restrict__ slots, int C,
+                                            int c0, double* red, double* tot) {
+  constexpr int E = 16 * W;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = (int)acc[0] + (int)acc[1];
-  double p[4][W];
+  if (lane < E && c0 + lane / W < C) {
+    const double* base = slots + (size_t)c0 * W + lane;
+    const size_t stride = (size_t)C * W;
+    double s = 0.0;
+    for (int k0 = w; k0 < n; k0 += 16 * kFinWaves) {
+      double v[16];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+      for (int i = 0; i < 16; ++i) {
+        const int k = k0 + i * kFinWaves;
+        v[i] = k < n ? base[(size_t)k * stride] : 0.0;
+      }
 #pragma unroll
-    for (int j = 0; j < W; ++j) p[q][j] = 0.0;
-  int k = s;
-  for (; k + 48 < n; k += 64)
+      for (int i = 0; i < 16; ++i) s += v[i];
+    }
+    red[w * E + lane] = s;
+  } else if (lane < E) {
+    red[w * E + lane] = 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x < E) {
+    double t = 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < W; ++j) p[q][j] += slots[((size_t)(k + 16 * q) * C + c) * W + j];
-#pragma unroll
-  for (int q = 0; q < 3; ++q)  // the tail: at most three slots left (k + 48 >= n)
-    if (k + 16 * q < n)
-#pragma unroll
-      for (int j = 0; j < W; ++j) p[q][j] += slots[((size_t)(k + 16 * q) * C + c) * W + j];
-#pragma unroll
-  for (int j = 0; j < W; ++j) out[j] = (p[0][j] + p[1][j]) + (p[2][j] + p[3][j]);
+    for (int k = 0; k < kFinWaves; ++k) t += red[k * E + threadIdx.x];
+    tot[threadIdx.x] = t;
+  }
+  __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
-                                                          const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* running_mean,
-                                                          float* running_var, float momentum, float eps, float* scale,
-                                                          float* shift, float* save_mean, float* save_invstd,
-                                                          long long rep) {
-  const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
-  if (c >= C) return;  // whole 16-lane groups leave together
-  double v[3];
-  lane_slots<3>(acc, bn_fwd_slots(acc), C, c, s, v);
-  const double S = sum16(v[0]), Q = sum16(v[1]), R = sum16(v[2]);
-  if (s != 0) return;
+__global__ __launch_bounds__(kFinThreads) void bn_finalize_kernel(double* __restrict__ acc, long long rows, int C,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ beta, float* running_mean,
+                                                                  float* running_var, float momentum, float eps,
+                                                                  float* scale, float* shift, float* save_mean,
+                                                                  float* save_invstd, long long rep) {
+  __shared__ double red[kFinWaves * 48], tot[48];
+  const int c0 = blockIdx.x * 16;
+  slot_sums16<3>(acc, bn_fwd_slots(acc), C, c0, red, tot);
+  const int c = c0 + (int)threadIdx.x;
+  if (threadIdx.x >= 16 || c >= C) return;
+  const double S = tot[threadIdx.x * 3], Q = tot[threadIdx.x * 3 + 1], R = tot[threadIdx.x * 3 + 2];
   const double n = (double)rows;
   const double mean = S / n;
   double m2 = Q + (R - S * mean);
@@ -262,37 +269,38 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   }
 }
 
-// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2 from the slots of workspace acc.
-// 16 lanes per channel (as bn_finalize_kernel); lane s of channel c's group.
-__device__ __forceinline__ void bn_bwd_finalize_one(double* __restrict__ acc, int C, int c, int s, double inv_rows,
-                                                    float* dgamma, float* dbeta, float* k1, float* k2) {
-  double v[2];
-  lane_slots<2>(acc, bn_bwd_slots(acc, C), C, c, s, v);
-  const double a = sum16(v[0]), b = sum16(v[1]);
-  if (s != 0) return;
+// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2 of channels [c0, c0 + 16) from the slots
+// of workspace acc (slot_sums16; every thread of the block calls it)
+__device__ __forceinline__ void bn_bwd_finalize16(double* __restrict__ acc, int C, int c0, double inv_rows,
+                                                  float* dgamma, float* dbeta, float* k1, float* k2) {
+  __shared__ double red[kFinWaves * 32], tot[32];
+  slot_sums16<2>(acc, bn_bwd_slots(acc, C), C, c0, red, tot);
+  const int c = c0 + (int)threadIdx.x;
+  if (threadIdx.x >= 16 || c >= C) return;
+  const double a = tot[threadIdx.x * 2], b = tot[threadIdx.x * 2 + 1];
   if (dbeta) dbeta[c] += (float)a;
   if (dgamma) dgamma[c] += (float)b;
   k1[c] = (float)(a * inv_rows);
   k2[c] = (float)(b * inv_rows);
 }
 
-// launch: 16 channels per 256-thread block
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
-                                                              float* dgamma, float* dbeta, float* k1, float* k2) {
-  const int c = blockIdx.x * 16 + (threadIdx.x >> 4);
-  if (c < C) bn_bwd_finalize_one(acc, C, c, threadIdx.x & 15, inv_rows, dgamma, dbeta, k1, k2);
+// launch: kFinThreads threads per 16 channels
+__global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
+                                                                      float* dgamma, float* dbeta, float* k1, float* k2) {
+  bn_bwd_finalize16(acc, C, blockIdx.x * 16, inv_rows, dgamma, dbeta, k1, k2);
 }
 
-// both BNs of a first block in one launch: channel groups [0, C) the first, [C, 2C) the second
-__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(double* __restrict__ acc, double* __restrict__ acc2,
-                                                               int C, double inv_rows, float* dgamma, float* dbeta,
-                                                               float* k1, float* k2, float* dgamma2, float* dbeta2,
-                                                               float* k1b, float* k2b) {
-  const int c = blockIdx.x * 16 + (threadIdx.x >> 4), s = threadIdx.x & 15;
-  if (c < C)
-    bn_bwd_finalize_one(acc, C, c, s, inv_rows, dgamma, dbeta, k1, k2);
-  else if (c < 2 * C)
-    bn_bwd_finalize_one(acc2, C, c - C, s, inv_rows, dgamma2, dbeta2, k1b, k2b);
+// both BNs of a first block in one launch: blocks [0, G) the first BN's 16-channel groups, [G, 2G) the second's
+__global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize2_kernel(double* __restrict__ acc, double* __restrict__ acc2,
+                                                                       int C, double inv_rows, float* dgamma,
+                                                                       float* dbeta, float* k1, float* k2,
+                                                                       float* dgamma2, float* dbeta2, float* k1b,
+                                                                       float* k2b) {
+  const int G = (C + 15) / 16;
+  if ((int)blockIdx.x < G)
+    bn_bwd_finalize16(acc, C, blockIdx.x * 16, inv_rows, dgamma, dbeta, k1, k2);
+  else
+    bn_bwd_finalize16(acc2, C, (blockIdx.x - G) * 16, inv_rows, dgamma2, dbeta2, k1b, k2b);
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
@@ -602,12 +610,40 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
     const int t = threadIdx.x + kStemBwdThreads * j;
     if (t < items) cx[j] = *reinterpret_cast<const u32x4*>(c + (img_row0 * W) * C + (size_t)t * 8);
   }
-  for (int k = 0; k < (p_next ? 2 : 1); ++k) {
-    const size_t prow = (size_t)n * P + p + k;
-    const u32x4* sg = reinterpret_cast<const u32x4*>(gy + prow * Q * C);
-    const u32x4* si = reinterpret_cast<const u32x4*>(idx + prow * Q * C);
-    for (int t = threadIdx.x; t < rowg / 16; t += kStemBwdThreads) reinterpret_cast<u32x4*>(lg + k * Q * C)[t] = sg[t];
-    for (int t = threadIdx.x; t < rowi / 16; t += kStemBwdThreads) reinterpret_cast<u32x4*>(li + k * rowi)[t] = si[t];
+  // the thread's 8 channels are the same for all its items (kStemBwdThreads is a multiple of C / 8): their
+  // per-channel constants are loaded once, not per item (7 x 8 scalar loads per item were the kernel's
+  // vector-memory instruction stream)
+  const int c8 = threadIdx.x & (cv - 1);
+  float k_sc[8], k_sh[8], k_mu[8], k_is[8], k_k1[8], k_k2[8], k_gi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int ch = c8 * 8 + e;
+    k_sc[e] = scale[ch];
+    k_sh[e] = shift[ch];
+    k_mu[e] = mean[ch];
+    k_is[e] = invstd[ch];
+    k_k1[e] = k1[ch];
+    k_k2[e] = k2[ch];
+    k_gi[e] = gamma[ch] * k_is[e];
+  }
+  // stage the (<= 2) pooled rows of gy and argmax: every load issued before any LDS store
+  const int ng = rowg / 16, ni = rowi / 16, nrows = p_next ? 2 : 1, nst = nrows * (ng + ni);
+  constexpr int kStage = 4;
+  u32x4 sv[kStage];
+  const u32x4* sg = reinterpret_cast<const u32x4*>(gy + ((size_t)n * P + p) * Q * C);
+  const u32x4* si = reinterpret_cast<const u32x4*>(idx + ((size_t)n * P + p) * Q * C);
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    const int t = threadIdx.x + kStemBwdThreads * j;
+    if (t < nst) sv[j] = t < nrows * ng ? sg[t] : si[t - nrows * ng];  // consecutive pooled rows are contiguous
+  }
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    const int t = threadIdx.x + kStemBwdThreads * j;
+    if (t < nst) {
+      char* dst = t < nrows * ng ? lds + (size_t)t * 16 : lds + 2 * rowg + (size_t)(t - nrows * ng) * 16;
+      *reinterpret_cast<u32x4*>(dst) = sv[j];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -616,7 +652,7 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
     if (t >= items) break;
     const int r = t >= items_row ? 1 : 0;  // input row 2p + r
     const int tw = t - r * items_row;
-    const int w = tw >> cvs, c8 = tw & (cv - 1);
+    const int w = tw >> cvs;
     // window row of (2p + r) in pooled row p: kh0 = 1 + r; in pooled row p + 1 (odd rows only): kh0 - 2
     const int kh0 = 1 + r;
     const bool p_two = r == 1 && p_next;
@@ -654,10 +690,9 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
     unpack8(cx[j], xx);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int ch = c8 * 8 + e;
-      gg[e] = __builtin_fmaf(xx[e], scale[ch], shift[ch]) > 0.f ? gg[e] : 0.f;
-      const float xh = (xx[e] - mean[ch]) * invstd[ch];
-      o[e] = gamma[ch] * invstd[ch] * (gg[e] - k1[ch] - xh * k2[ch]);
+      gg[e] = __builtin_fmaf(xx[e], k_sc[e], k_sh[e]) > 0.f ? gg[e] : 0.f;
+      const float xh = (xx[e] - k_mu[e]) * k_is[e];
+      o[e] = k_gi[e] * (gg[e] - k_k1[e] - xh * k_k2[e]);
     }
     *reinterpret_cast<u32x4*>(gc + xo) = pack8(o);
   }
@@ -691,7 +726,7 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
   hipStream_t st = (hipStream_t)stream;
   if (diag_skip(1, st)) return AVT_OK;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, rows, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }
@@ -706,7 +741,7 @@ extern "C" int avt_bn_finalize_rep(double* acc, long long rows, long long rep, i
                                    void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize_rep: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0 && rep >= 1, "bn_finalize_rep: empty input");
-  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, rep);
   return check_launch("bn_finalize_rep");
 }
@@ -795,7 +830,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.C = C;
   if (t2) {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
-    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((2 * C + 15) / 16), dim3(256), 0, st, acc, acc2, C, inv_rows,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + 15) / 16)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
     p.mean2 = t2->mean;
@@ -807,7 +842,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
-    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, inv_rows, t1->dgamma,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   }
@@ -833,7 +868,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
                        rows, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
@@ -856,7 +891,7 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)gm, nullptr,
@@ -878,7 +913,7 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, nullptr, scale,
@@ -911,7 +946,8 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   AVT_REQUIRE(gy && idx && carg && c && scale && shift && mean && invstd && gamma && gc && workspace,
               "stem_maxpool_bn_relu_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "stem_maxpool_bn_relu_bwd: C=%d unsupported", C);
-  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)2 * W * (C / 8) <= 6 * kStemBwdThreads,
+  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)2 * W * (C / 8) <= 6 * kStemBwdThreads &&
+                  (long long)((W + 1) / 2 + 1) * C * 6 / 16 <= 4 * kStemBwdThreads,
               "stem_maxpool_bn_relu_bwd: W=%d C=%d too wide", W, C);
   AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_maxpool_bn_relu_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");
@@ -922,7 +958,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
                        (long long)N * P * Q, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, acc, C,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * ((H + 1) / 2)), dim3(kStemBwdThreads), (size_t)6 * Q * C,
                      st, (const bf16_t*)gy,

@@ -4,7 +4,7 @@
 // BN's ReLU and reduced into its backward statistics, so the separate reduction pass over
 // (g, y, xc) of the reference's BatchNorm2d backward (base_models.py:46-49, 58-67) is not needed:
 //   g' = g * [y > 0]  or  g * [fma(xc, scale, shift) > 0]          (the mask the forward produced)
-//   acc[slot][c] += (sum g', sum g' * (xc - mean) * invstd)        (fp64 atomics, slot = tile % SLOTS)
+//   acc[slot][c] = (sum g', sum g' * (xc - mean) * invstd)         (slot = the block's row tile, plain stores)
 // and g' is what gets stored (it is also the residual branch's gradient of an identity block).
 // Included by conv_gemm.hip inside namespace avt.
 #pragma once
@@ -29,9 +29,11 @@ __device__ __forceinline__ void epi_unpack8(const u32x4& v, float* f) {
 
 // NT threads; OCPR = BN / 8 16-byte chunks per tile row.  orow(r) -> output row of tile row r.
 // `scratch`: LDS of >= NW * BN * 3 floats that may overwrite Ct once every thread has read it.
+// mt / nrow_tiles: the block's row tile and the launch's row tiles -- the slot the block's columns n0 .. n0+BN-1
+// of the statistics go to (every column tile of a row tile writes its own columns of that one slot)
 template <int NT, int BM, int BN, int UMAX, typename OrowFn>
 __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t* Ct, int ct_ld, int n0, int rows_valid,
-                                             int tile_id, OrowFn orow, float* scratch) {
+                                             int mt, int nrow_tiles, OrowFn orow, float* scratch) {
   constexpr int OCPR = BN / 8;
   static_assert(NT % OCPR == 0 && 64 % OCPR == 0, "a thread keeps one channel chunk");
   const int tid = threadIdx.x;
@@ -144,14 +146,13 @@ __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t
     }
   }
   __syncthreads();
-  // this block's own slot (avt_common.h): the call's earlier launches' slots come first (bslot_base), and an
+  // this row tile's slot (avt_common.h): the call's earlier launches' slots come first (bslot_base), and an
   // appending call (a stride-2 block's downsample dgrad) starts after the slots of the call before it
-  (void)tile_id;
-  const int total = p.bslot_total ? p.bslot_total : (int)gridDim.x;
+  const int total = p.bslot_total ? p.bslot_total : nrow_tiles;
   bn_write_header(p.bacc, total, p.bappend);
   if (two) bn_write_header(p.bacc2, total, p.bappend);
-  const size_t slot = (size_t)(p.bslot_base + bn_slot_base(p.bacc, p.bappend) + (int)blockIdx.x);
-  const size_t slot2 = two ? (size_t)(p.bslot_base + bn_slot_base(p.bacc2, p.bappend) + (int)blockIdx.x) : 0;
+  const size_t slot = (size_t)(p.bslot_base + bn_slot_base(p.bacc, p.bappend) + mt);
+  const size_t slot2 = two ? (size_t)(p.bslot_base + bn_slot_base(p.bacc2, p.bappend) + mt) : 0;
   for (int c = tid; c < BN; c += NT) {
     float a = 0.f, b = 0.f, d = 0.f;
 #pragma unroll
@@ -176,7 +177,7 @@ __device__ __forceinline__ void epi_store_bn(const GemmNTParams& p, const bf16_t
 // footprint of their main loop (the BN epilogue's load groups would raise it and cost occupancy).
 template <int NT, int BM, int BN, bool EPI, typename OrowFn, int UMAX = 4>
 __device__ __forceinline__ void epi_store(const GemmNTParams& p, const bf16_t* Ct, int ct_ld, int n0, int rows_valid,
-                                          int tile_id, OrowFn orow, float* scratch) {
+                                          int mt, int nrow_tiles, OrowFn orow, float* scratch) {
   if constexpr (!EPI) {
     constexpr int OCPR = BN / 8;
     for (int idx = threadIdx.x; idx < BM * OCPR; idx += NT) {
@@ -200,6 +201,6 @@ __device__ __forceinline__ void epi_store(const GemmNTParams& p, const bf16_t* C
     }
     return;
   } else {
-    epi_store_bn<NT, BM, BN, UMAX>(p, Ct, ct_ld, n0, rows_valid, tile_id, orow, scratch);
+    epi_store_bn<NT, BM, BN, UMAX>(p, Ct, ct_ld, n0, rows_valid, mt, nrow_tiles, orow, scratch);
   }
 }

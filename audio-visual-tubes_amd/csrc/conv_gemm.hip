@@ -36,8 +36,8 @@ struct GemmNTParams {
   // result g (after `add`) is masked by the ReLU of the BN that produced the positions' activations,
   // g' = g * [by > 0] (by given: the block output) or g * [fma(bx, scale, shift) > 0] (BasicBlock.bn1),
   // stored as g', and that BN's backward reductions (sum g', sum g' * xhat), xhat = (bx - mean)*invstd,
-  // are stored into slot bslot_base (+ bacc's header[0] when bappend) + blockIdx.x of bacc (avt_common.h;
-  // bslot_total: the slots of all launches of this call, 0 = gridDim.x); bx2/bst2/bacc2 optionally a second BN fed
+  // are stored into slot bslot_base (+ bacc's header[0] when bappend) + the block's row tile of bacc (avt_common.h;
+  // bslot_total: the slots of all launches of this call, 0 = this launch's row tiles); bx2/bst2/bacc2 optionally a second BN fed
   // by the same g' (the downsample BN of a first block: bn2 and downsample.1 share the ReLU).
   const bf16_t* bx;
   const bf16_t* by;
@@ -818,15 +818,15 @@ static void launch_glds(const GemmNTParams& p, hipStream_t st) {
         // K loop: its rows are written as 0 (+ add) -- or, accumulating in place (add == out), are
         // already final and are skipped
         if (tc.ntaps == 0 && p.add != nullptr && p.add == p.out) continue;
-        const int grid = ((pc.M + BMc - 1) / BMc) * (p.Ng / BNc);
-        if (grid <= 0) continue;
+        const int rtiles = (pc.M + BMc - 1) / BMc;  // the class's row tiles = its statistic slots
+        if (rtiles * (p.Ng / BNc) <= 0) continue;
         if (pass == 0) {
-          if (pc.bx != nullptr) ep_total += grid;
+          if (pc.bx != nullptr) ep_total += rtiles;
           continue;
         }
         pc.bslot_base = ep_base;
         pc.bslot_total = ep_total;
-        if (pc.bx != nullptr) ep_base += grid;
+        if (pc.bx != nullptr) ep_base += rtiles;
         launch_pipe_one<MODE, WM, WN, TM, TN, NST, BK>(pc, tc, st);
       }
 }
@@ -1732,30 +1732,35 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
     if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
   }
   if (slab && !diag_skip(4, st)) {
-    const long long n4 = (long long)pl.p.Mg * pl.p.Ng / 4;
-    long long blocks = (n4 + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    // waves per 64 slab positions: the largest power of two <= min(splits, kRedWaves)
+    int G = 1;
+    while (G * 2 <= pl.splits && G * 2 <= kRedWaves) G *= 2;
+    const int ngrp = kRedWaves / G;
+    const int wm = BM == 256 ? 4 : 2, wn = 2, tm = BM == 64 ? 1 : 2, tn = BN == 256 ? 4 : BN == 128 ? 2 : 1;
+    const long long per_tile = (long long)wm * wn * tm * tn * 4 * 64;
+    long long blocks = ((long long)pl.tiles * per_tile + 64LL * ngrp - 1) / (64LL * ngrp);
+    if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     const int nnt = pl.p.Ng / BN, ldw = R * S * Creal;
-    const dim3 g((unsigned)blocks), b(256);
+    const dim3 g((unsigned)blocks), b(kRedWaves * 64);
     if (BM == 256 && BN == 256)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<4, 2, 2, 4>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
     else if (BM == 256)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<4, 2, 2, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
     else if (BM == 128 && BN == 128)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 2, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
     else if (BM == 128)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 2, 1>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
     else if (BN == 128)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 1, 2>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
     else
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<2, 2, 1, 1>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
-                         pl.p.Mg, ldw, dw);
+                         pl.p.Mg, ldw, G, dw);
   }
   return check_launch("conv2d_wgrad");
 }

@@ -428,6 +428,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       for (int v = 0; v < AV; ++v) Ct[acc_row(i, v) * CT_LD + wn * (BN / WN) + j * FR + frow] = f2bf(acc[i][j][v]);
   __syncthreads();
   if (!HALO_DBG(16))
-    epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, [&](int r) -> size_t { return (size_t)(m0 + r); },
+    epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, mt, (p.M + BM - 1) / BM,
+                               [&](int r) -> size_t { return (size_t)(m0 + r); },
                         reinterpret_cast<float*>(smem));
 }

@@ -377,5 +377,6 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     const int oh = rem / p.OW, ow = rem - oh * p.OW;
     return ((size_t)n * ta.OHf + 2 * oh + cph) * ta.OWf + 2 * ow + cpw;
   };
-  epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, bid, orow, reinterpret_cast<float*>(smem));
+  epi_store<NT, BM, BN, EPI>(p, Ct, CT_LD, n0, rows_valid, mt, (p.M + BM - 1) / BM, orow,
+                             reinterpret_cast<float*>(smem));
 }

@@ -308,39 +308,65 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
   }
 }
 
-// DW += sum over splits of the register-order partial tiles of conv_tn_pipe_kernel<WM, WN, TM, TN, *>:
-// one thread per (tile, wave, i, j, quarter, lane) float4 -- 16-B coalesced slab reads, and four DW
-// read-modify-writes (rows r0 .. r0+3 of one column; 32 consecutive columns per half-wave)
+// DW += sum over splits of the register-order partial tiles of conv_tn_pipe_kernel<WM, WN, TM, TN, *>, in a
+// fixed order with all of a position's splits in flight at once: a block of kRedWaves waves covers
+// 64 * kRedWaves / G consecutive float4 positions of a split's slab, G waves per 64 of them (one position per
+// lane); wave j of a group adds splits j, j + G, j + 2G, ... in turn (8 loads in flight per batch) and the
+// group's G partials meet in LDS in wave order.  G = a power of two <= min(splits, kRedWaves), fixed per shape.
+// Each position then makes four DW read-modify-writes (rows r0 .. r0+3 of one column; 32 consecutive columns
+// per half-wave).
+constexpr int kRedWaves = 16;
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256) void wgrad_slab_reduce_native_kernel(const float* __restrict__ slab, int splits,
-                                                                       int ntiles, int nnt, int Mg, int ldw,
-                                                                       float* __restrict__ dw) {
+__global__ __launch_bounds__(kRedWaves * 64) void wgrad_slab_reduce_native_kernel(const float* __restrict__ slab,
+                                                                                 int splits, int ntiles, int nnt,
+                                                                                 int Mg, int ldw, int G,
+                                                                                 float* __restrict__ dw) {
   constexpr int NW = WM * WN, BM = WM * TM * 32, BN = WN * TN * 32;
-  constexpr int PER_TILE = NW * TM * TN * 4 * 64;  // float4s per tile
+  constexpr int PER_TILE = NW * TM * TN * 4 * 64;  // float4s per tile (a multiple of 64)
+  __shared__ f32x4 red[kRedWaves][64];
   const long long total = (long long)ntiles * PER_TILE;
-  const long long split_stride = total;
-  for (long long f = blockIdx.x * (long long)blockDim.x + threadIdx.x; f < total;
-       f += (long long)gridDim.x * blockDim.x) {
-    f32x4 a = reinterpret_cast<const f32x4*>(slab)[f];
-    for (int s = 1; s < splits; ++s) a += reinterpret_cast<const f32x4*>(slab)[f + s * split_stride];
-    const int lane = (int)(f & 63);
-    long long r = f >> 6;
-    const int q = (int)(r & 3);
-    r >>= 2;
-    const int j = (int)(r % TN);
-    r /= TN;
-    const int i = (int)(r % TM);
-    r /= TM;
-    const int wid = (int)(r % NW);
-    const int tile = (int)(r / NW);
-    const int mt = tile / nnt, nt = tile - mt * nnt;
-    const int wm = wid / WN, wn = wid % WN;
-    const int col = nt * BN + wn * (BN / WN) + j * 32 + (lane & 31);
-    const int r0 = mt * BM + wm * (BM / WM) + i * 32 + 8 * q + 4 * (lane >> 5);
-    if (col < ldw) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int grp = w / G, j = w - grp * G, ngrp = kRedWaves / G;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  for (long long f0 = (long long)blockIdx.x * 64 * ngrp; f0 < total; f0 += (long long)gridDim.x * 64 * ngrp) {
+    const long long f = f0 + (long long)grp * 64 + lane;
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    if (f < total) {
+      for (int s0 = j; s0 < splits; s0 += 8 * G) {
+        f32x4 v[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (r0 + e < Mg) dw[(size_t)(r0 + e) * ldw + col] += a[e];
+        for (int i = 0; i < 8; ++i) {
+          const int sp = s0 + i * G;
+          v[i] = sp < splits ? s4[f + sp * total] : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a += v[i];
+      }
     }
+    red[w][lane] = a;
+    __syncthreads();
+    if (j == 0 && f < total) {
+      f32x4 t = red[w][lane];
+      for (int k = 1; k < G; ++k) t += red[w + k][lane];
+      long long r = f >> 6;
+      const int q = (int)(r & 3);
+      r >>= 2;
+      const int jj = (int)(r % TN);
+      r /= TN;
+      const int i = (int)(r % TM);
+      r /= TM;
+      const int wid = (int)(r % NW);
+      const int tile = (int)(r / NW);
+      const int mt = tile / nnt, nt = tile - mt * nnt;
+      const int wm = wid / WN, wn = wid % WN;
+      const int col = nt * BN + wn * (BN / WN) + jj * 32 + (lane & 31);
+      const int r0 = mt * BM + wm * (BM / WM) + i * 32 + 8 * q + 4 * (lane >> 5);
+      if (col < ldw) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (r0 + e < Mg) dw[(size_t)(r0 + e) * ldw + col] += t[e];
+      }
+    }
+    __syncthreads();
   }
 }

@@ -420,7 +420,7 @@ class _HardWayAttentionFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gA, glogits):
-        from ._lib import call
+        from ._lib import call, query
         from .trunk import P, stream_ptr
 
         if gA is None and glogits is None:

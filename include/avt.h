@@ -78,7 +78,8 @@ int avt_copy16(void* dst, const void* src, size_t bytes, int blocks, void* strea
 /* ---- convolution (implicit GEMM on bf16 MFMA, fp32 accumulate) ---- */
 /* BatchNorm statistics (deterministic).  A BN's fp64 accumulator holds a small header and one slot of
  * partial sums per row tile (or persistent block / reduce block) of the launch that accumulates it, each
- * slot written by exactly one block with plain stores -- no atomics, nothing to zero between uses, any
+ * slot element written by exactly one block with plain stores (the column tiles of a row tile write
+ * disjoint channel ranges of its slot) -- no atomics, nothing to zero between uses, any
  * contents on entry.  The finalize sums the slots in slot order, so identical inputs give bitwise identical
  * statistics, gradients and updates on every run (model.py:112-154's CPU path is deterministic too).
  * Forward: avt_bn_acc_doubles(rows, C) doubles; backward: avt_bn_bwd_workspace(rows, C) bytes.

@@ -2,7 +2,7 @@
 
     python tools/timeline.py <run_kernel_trace.csv> [--top 30] [--step -1]
 
-Steps are delimited by adam_kernel launches; the replayed steps are the shortest ones.  For the
+Steps are delimited by adam_prep_kernel launches (one per step); the replayed steps are the shortest ones.  For the
 chosen step (default: the median replayed step) prints the wall time, the time with no kernel
 running (gaps), the time with exactly one kernel running attributed to that kernel ("alone" = the
 serial critical path the other stream did not cover), and the overlapped time.
@@ -30,11 +30,13 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r[2]]
+    # one adam_prep_kernel per train step (Adam itself runs once per trunk region)
+    mark = "adam_prep_kernel" if any("adam_prep_kernel" in r[2] for r in rows) else "adam_kernel"
+    ends = [i for i, r in enumerate(rows) if mark in r[2]]
     steps = []
     for a, b in zip(ends, ends[1:]):
-        seg = rows[a + 1:b + 1]
-        t0 = rows[a][1]
+        seg = rows[a:b]
+        t0 = rows[a][0]
         t1 = max(r[1] for r in seg)
         steps.append((t1 - t0, seg, t0))
     if not steps:
