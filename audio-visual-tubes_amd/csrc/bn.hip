@@ -36,7 +36,7 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 }
 
 // The slot sums of 16 consecutive channels [c0, c0 + 16), W statistics each, in a fixed order: wave w of the
-// block adds slots w, w + kFinWaves, w + 2 kFinWaves, ... in turn (16 independent loads in flight per
+// block adds slots w, w + kFinWaves, w + 2 kFinWaves, ... in turn (32 independent loads in flight per
 // batch); lane l < 16 W owns element l = (channel c0 + l / W, statistic l % W) of a slot's 16-channel run, so a
 // slot is one coalesced 8 B/lane load.  The waves' partials meet in LDS in wave order; tot[l] on return
 // (after a barrier).  Launch: kFinThreads threads per 16 channels.
@@ -51,15 +51,15 @@ __device__ __forceinline__ void slot_sums16(const double* __restrict__ acc, cons
     const double* base = slots + (size_t)c0 * W + lane;
     const size_t stride = (size_t)C * W;
     double s = 0.0;
-    for (int k0 = w; k0 < n; k0 += 16 * kFinWaves) {
-      double v[16];
+    for (int k0 = w; k0 < n; k0 += 32 * kFinWaves) {  // one batch for up to 512 slots
+      double v[32];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const int k = k0 + i * kFinWaves;
         v[i] = k < n ? base[(size_t)k * stride] : 0.0;
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s += v[i];
+      for (int i = 0; i < 32; ++i) s += v[i];
     }
     red[w * E + lane] = s;
   } else if (lane < E) {
@@ -605,15 +605,28 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
   constexpr int kItems = 6;
   u32x4 cx[kItems];
   const size_t img_row0 = (size_t)n * H + 2 * p;  // input row 2p of image n
+  // item t -> (input row 2p + r, pixel w, the thread's channel chunk): per row the even pixels first, then the
+  // odd ones, so that a wave's items share their candidate-window pattern (even h / w: one window row / column,
+  // odd: two) and the absent candidates are skipped by wave-uniform branches
+  const int cw = threadIdx.x & (cv - 1), we_items = ((W + 1) >> 1) * cv;
+  auto item_pix = [&](int t, int& r, int& w) {
+    r = t >= items_row ? 1 : 0;
+    const int tw = t - r * items_row;
+    w = tw < we_items ? 2 * (tw >> cvs) : 2 * ((tw - we_items) >> cvs) + 1;
+  };
 #pragma unroll
   for (int j = 0; j < kItems; ++j) {
     const int t = threadIdx.x + kStemBwdThreads * j;
-    if (t < items) cx[j] = *reinterpret_cast<const u32x4*>(c + (img_row0 * W) * C + (size_t)t * 8);
+    if (t < items) {
+      int r, w;
+      item_pix(t, r, w);
+      cx[j] = *reinterpret_cast<const u32x4*>(c + ((img_row0 + r) * W + w) * C + cw * 8);
+    }
   }
   // the thread's 8 channels are the same for all its items (kStemBwdThreads is a multiple of C / 8): their
   // per-channel constants are loaded once, not per item (7 x 8 scalar loads per item were the kernel's
   // vector-memory instruction stream)
-  const int c8 = threadIdx.x & (cv - 1);
+  const int c8 = cw;
   float k_sc[8], k_sh[8], k_mu[8], k_is[8], k_k1[8], k_k2[8], k_gi[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -650,41 +663,29 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
   for (int j = 0; j < kItems; ++j) {
     const int t = threadIdx.x + kStemBwdThreads * j;
     if (t >= items) break;
-    const int r = t >= items_row ? 1 : 0;  // input row 2p + r
-    const int tw = t - r * items_row;
-    const int w = tw >> cvs;
-    // window row of (2p + r) in pooled row p: kh0 = 1 + r; in pooled row p + 1 (odd rows only): kh0 - 2
-    const int kh0 = 1 + r;
-    const bool p_two = r == 1 && p_next;
-    const int k1r = p_two ? 1 : 0;  // LDS row of the second window row (aliases the first if none)
-    const int q0 = w >> 1, kw0 = w - 2 * q0 + 1;
-    const bool q_two = (w & 1) && q0 + 1 < Q;
-    const int q1 = q_two ? q0 + 1 : q0;
-    const int e00 = q0 * C + c8 * 8, e01 = q1 * C + c8 * 8;
-    const int e10 = k1r * Q * C + e00, e11 = k1r * Q * C + e01;
-    const unsigned long long i00 = *reinterpret_cast<const unsigned long long*>(li + e00);
-    const unsigned long long i01 = *reinterpret_cast<const unsigned long long*>(li + e01);
-    const unsigned long long i10 = *reinterpret_cast<const unsigned long long*>(li + e10);
-    const unsigned long long i11 = *reinterpret_cast<const unsigned long long*>(li + e11);
-    // window position of (h, w) in each candidate; 0xff (never an argmax) where there is none
-    const int pos00 = kh0 * 3 + kw0;
-    const int pos01 = q_two ? kh0 * 3 + kw0 - 2 : 0xff;
-    const int pos10 = p_two ? (kh0 - 2) * 3 + kw0 : 0xff;
-    const int pos11 = (p_two && q_two) ? (kh0 - 2) * 3 + kw0 - 2 : 0xff;
-    float gg[8], xx[8], o[8], f00[8], f01[8], f10[8], f11[8];
-    unpack8(*reinterpret_cast<const u32x4*>(lg + e00), f00);
-    unpack8(*reinterpret_cast<const u32x4*>(lg + e01), f01);
-    unpack8(*reinterpret_cast<const u32x4*>(lg + e10), f10);
-    unpack8(*reinterpret_cast<const u32x4*>(lg + e11), f11);
+    int r, w;
+    item_pix(t, r, w);
+    // window row of (2p + r) in pooled row p: kh0 = 1 + r; in pooled row p + 1 (odd rows only): kh0 - 2;
+    // column: q0 = w / 2 at kw0 (1 for even w, 2 for odd) and, odd w only, q0 + 1 at kw0 - 2
+    const int kh0 = 1 + r, q0 = w >> 1, kw0 = (w & 1) + 1;
+    const bool p_two = r == 1 && p_next, q_two = (w & 1) && q0 + 1 < Q;
+    float gg[8], xx[8], o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int sh8 = 8 * e;
-      float a = 0.f;
-      a += ((int)((i00 >> sh8) & 0xff) == pos00) ? f00[e] : 0.f;
-      a += ((int)((i01 >> sh8) & 0xff) == pos01) ? f01[e] : 0.f;
-      a += ((int)((i10 >> sh8) & 0xff) == pos10) ? f10[e] : 0.f;
-      a += ((int)((i11 >> sh8) & 0xff) == pos11) ? f11[e] : 0.f;
-      gg[e] = a;
+    for (int e = 0; e < 8; ++e) gg[e] = 0.f;
+    // g' += gy of a candidate window whose argmax is (h, w), in the order (p, q0), (p, q0+1), (p+1, q0), (p+1, q0+1)
+    auto cand = [&](int lrow, int q, int pos) {
+      const int el = lrow * Q * C + q * C + c8 * 8;
+      const unsigned long long iv = *reinterpret_cast<const unsigned long long*>(li + el);
+      float f[8];
+      unpack8(*reinterpret_cast<const u32x4*>(lg + el), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gg[e] += ((int)((iv >> (8 * e)) & 0xff) == pos) ? f[e] : 0.f;
+    };
+    cand(0, q0, kh0 * 3 + kw0);
+    if (q_two) cand(0, q0 + 1, kh0 * 3 + kw0 - 2);
+    if (p_two) {
+      cand(1, q0, (kh0 - 2) * 3 + kw0);
+      if (q_two) cand(1, q0 + 1, (kh0 - 2) * 3 + kw0 - 2);
     }
     const size_t xo = ((img_row0 + r) * W + w) * C + c8 * 8;
     unpack8(cx[j], xx);

@@ -1732,17 +1732,17 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
     if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
   }
   if (slab && !diag_skip(4, st)) {
-    // waves per 64 slab positions: the largest power of two <= min(splits, kRedWaves)
-    int G = 1;
-    while (G * 2 <= pl.splits && G * 2 <= kRedWaves) G *= 2;
-    const int ngrp = kRedWaves / G;
+    // G waves per 64 slab positions: 1 where the positions alone give ~64 K threads, else up to min(splits, 16)
     const int wm = BM == 256 ? 4 : 2, wn = 2, tm = BM == 64 ? 1 : 2, tn = BN == 256 ? 4 : BN == 128 ? 2 : 1;
-    const long long per_tile = (long long)wm * wn * tm * tn * 4 * 64;
-    long long blocks = ((long long)pl.tiles * per_tile + 64LL * ngrp - 1) / (64LL * ngrp);
-    if (blocks > 2048) blocks = 2048;
+    const long long positions = (long long)pl.tiles * wm * wn * tm * tn * 4 * 64;
+    int G = 1;
+    while (G * 2 <= pl.splits && G * 2 <= 16 && positions * G < 65536) G *= 2;
+    const int nwb = G > 4 ? G : 4, ngrp = nwb / G;
+    long long blocks = (positions + 64LL * ngrp - 1) / (64LL * ngrp);
+    if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
     const int nnt = pl.p.Ng / BN, ldw = R * S * Creal;
-    const dim3 g((unsigned)blocks), b(kRedWaves * 64);
+    const dim3 g((unsigned)blocks), b(nwb * 64);
     if (BM == 256 && BN == 256)
       hipLaunchKernelGGL((wgrad_slab_reduce_native_kernel<4, 2, 2, 4>), g, b, 0, st, slab, pl.splits, pl.tiles, nnt,
                          pl.p.Mg, ldw, G, dw);

@@ -309,24 +309,21 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
 }
 
 // DW += sum over splits of the register-order partial tiles of conv_tn_pipe_kernel<WM, WN, TM, TN, *>, in a
-// fixed order with all of a position's splits in flight at once: a block of kRedWaves waves covers
-// 64 * kRedWaves / G consecutive float4 positions of a split's slab, G waves per 64 of them (one position per
-// lane); wave j of a group adds splits j, j + G, j + 2G, ... in turn (8 loads in flight per batch) and the
-// group's G partials meet in LDS in wave order.  G = a power of two <= min(splits, kRedWaves), fixed per shape.
-// Each position then makes four DW read-modify-writes (rows r0 .. r0+3 of one column; 32 consecutive columns
-// per half-wave).
-constexpr int kRedWaves = 16;
+// fixed order with a position's splits in flight together: G waves (a power of two, fixed per shape; > 1 only
+// where the slab has too few positions to fill the chip: many splits of few tiles) share 64 consecutive float4
+// positions, one per lane; wave j of the G adds splits j, j + G, j + 2G, ... in turn (8 loads in flight per
+// batch) and the G partials meet in LDS in wave order.  blockDim = 64 * max(4, G).  Each position then makes
+// four DW read-modify-writes (rows r0 .. r0+3 of one column; 32 consecutive columns per half-wave).
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(kRedWaves * 64) void wgrad_slab_reduce_native_kernel(const float* __restrict__ slab,
-                                                                                 int splits, int ntiles, int nnt,
-                                                                                 int Mg, int ldw, int G,
-                                                                                 float* __restrict__ dw) {
+__global__ __launch_bounds__(1024) void wgrad_slab_reduce_native_kernel(const float* __restrict__ slab, int splits,
+                                                                       int ntiles, int nnt, int Mg, int ldw, int G,
+                                                                       float* __restrict__ dw) {
   constexpr int NW = WM * WN, BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int PER_TILE = NW * TM * TN * 4 * 64;  // float4s per tile (a multiple of 64)
-  __shared__ f32x4 red[kRedWaves][64];
+  __shared__ f32x4 red[16][64];
   const long long total = (long long)ntiles * PER_TILE;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int grp = w / G, j = w - grp * G, ngrp = kRedWaves / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwb = blockDim.x >> 6;
+  const int grp = w / G, j = w - grp * G, ngrp = nwb / G;
   const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
   for (long long f0 = (long long)blockIdx.x * 64 * ngrp; f0 < total; f0 += (long long)gridDim.x * 64 * ngrp) {
     const long long f = f0 + (long long)grp * 64 + lane;
@@ -343,11 +340,13 @@ __global__ __launch_bounds__(kRedWaves * 64) void wgrad_slab_reduce_native_kerne
         for (int i = 0; i < 8; ++i) a += v[i];
       }
     }
-    red[w][lane] = a;
-    __syncthreads();
+    if (G > 1) {  // block-uniform
+      red[w][lane] = a;
+      __syncthreads();
+      if (j == 0)
+        for (int k = 1; k < G; ++k) a += red[w + k][lane];
+    }
     if (j == 0 && f < total) {
-      f32x4 t = red[w][lane];
-      for (int k = 1; k < G; ++k) t += red[w + k][lane];
       long long r = f >> 6;
       const int q = (int)(r & 3);
       r >>= 2;
@@ -364,9 +363,9 @@ __global__ __launch_bounds__(kRedWaves * 64) void wgrad_slab_reduce_native_kerne
       if (col < ldw) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (r0 + e < Mg) dw[(size_t)(r0 + e) * ldw + col] += t[e];
+          if (r0 + e < Mg) dw[(size_t)(r0 + e) * ldw + col] += a[e];
       }
     }
-    __syncthreads();
+    if (G > 1) __syncthreads();
   }
 }

@@ -275,7 +275,7 @@ __device__ __forceinline__ unsigned peak_hash(unsigned x) {
 }
 
 template <int SHAPE>  // 0: v_mfma_f32_32x32x16_bf16 (4 accumulators), 1: v_mfma_f32_16x16x32_bf16 (8)
-__global__ __launch_bounds__(256) void peak_mfma_kernel(float* __restrict__ sink, int iters, unsigned seed) {
+__global__ __launch_bounds__(1024) void peak_mfma_kernel(float* __restrict__ sink, int iters, unsigned seed) {
   const unsigned g = blockIdx.x * 256u + threadIdx.x;
   bf16x8 a, b;
 #pragma unroll
@@ -292,6 +292,7 @@ __global__ __launch_bounds__(256) void peak_mfma_kernel(float* __restrict__ sink
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][v] = 0.f;
+#pragma nounroll
     for (int it = 0; it < iters; ++it)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
@@ -305,13 +306,14 @@ __global__ __launch_bounds__(256) void peak_mfma_kernel(float* __restrict__ sink
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int v = 0; v < 4; ++v) acc[i][v] = 0.f;
+    // (bounds of 1024 threads keep the accumulators in VGPRs: at 256 the allocator put them in AGPRs and
+    // rotated them through ~50 accvgpr moves per iteration, which halved the measured 16x16x32 rate)
+#pragma nounroll
     for (int it = 0; it < iters; ++it)
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) s += acc[i][v];
+    for (int i = 0; i < 8; ++i) s += (acc[i][0] + acc[i][1]) + (acc[i][2] + acc[i][3]);
   }
   sink[g] = s;  // keeps the loop live; one vector store per lane
 }
