@@ -35,41 +35,42 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
-// The slot sums of 16 consecutive channels [c0, c0 + 16), W statistics each, in a fixed order: wave w of the
-// block adds slots w, w + kFinWaves, w + 2 kFinWaves, ... in turn (32 independent loads in flight per
-// batch); lane l < 16 W owns element l = (channel c0 + l / W, statistic l % W) of a slot's 16-channel run, so a
-// slot is one coalesced 8 B/lane load.  The waves' partials meet in LDS in wave order; tot[l] on return
-// (after a barrier).  Launch: kFinThreads threads per 16 channels.
-constexpr int kFinWaves = 16, kFinThreads = kFinWaves * 64;
+// The slot sums of kFinCB consecutive channels [c0, c0 + kFinCB), W statistics each, in a fixed order.  A
+// slot's run of E = kFinCB * W doubles is contiguous; a wave-load covers SPI = 64 / E slots (lane = (slot
+// offset so, element e)), so wave w, lane (so, e) adds slots (i kFinWaves + w) SPI + so for i = 0, 1, ... in
+// turn, 8 loads in flight per batch (one round trip for up to 8 * kFinWaves * SPI slots: 1024 fwd / bwd);
+// the lanes' partials meet in LDS in (wave, slot offset) order.  tot[e] on return (after a barrier).
+// Launch: kFinThreads threads per kFinCB channels -- many small blocks, since a finalize is latency-bound.
+constexpr int kFinWaves = 16, kFinThreads = kFinWaves * 64, kFinCB = 4;
 template <int W>
-__device__ __forceinline__ void slot_sums16(const double* __restrict__ acc, const double* __restrict__ slots, int C,
-                                            int c0, double* red, double* tot) {
-  constexpr int E = 16 * W;
+__device__ __forceinline__ void slot_sums(const double* __restrict__ acc, const double* __restrict__ slots, int C,
+                                          int c0, double* red, double* tot) {
+  constexpr int E = kFinCB * W, SPI = 64 / E, STEP = kFinWaves * SPI;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int so = lane / E, e = lane - so * E;
   const int n = (int)acc[0] + (int)acc[1];
-  if (lane < E && c0 + lane / W < C) {
-    const double* base = slots + (size_t)c0 * W + lane;
-    const size_t stride = (size_t)C * W;
-    double s = 0.0;
-    for (int k0 = w; k0 < n; k0 += 32 * kFinWaves) {  // one batch for up to 512 slots
-      double v[32];
+  double s = 0.0;
+  if (so < SPI && c0 + e / W < C) {
+    const double* base = slots + (size_t)c0 * W + e;
+    const unsigned stride = (unsigned)(C * W);
+    for (int k0 = w * SPI + so; k0 < n; k0 += 8 * STEP) {
+      double v[8];
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const int k = k0 + i * kFinWaves;
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + i * STEP;
         v[i] = k < n ? base[(size_t)k * stride] : 0.0;
       }
 #pragma unroll
-      for (int i = 0; i < 32; ++i) s += v[i];
+      for (int i = 0; i < 8; ++i) s += v[i];
     }
-    red[w * E + lane] = s;
-  } else if (lane < E) {
-    red[w * E + lane] = 0.0;
   }
+  red[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x < E) {
     double t = 0.0;
+    for (int ww = 0; ww < kFinWaves; ++ww)
 #pragma unroll
-    for (int k = 0; k < kFinWaves; ++k) t += red[k * E + threadIdx.x];
+      for (int o = 0; o < SPI; ++o) t += red[ww * 64 + o * E + threadIdx.x];
     tot[threadIdx.x] = t;
   }
   __syncthreads();
@@ -81,11 +82,11 @@ __global__ __launch_bounds__(kFinThreads) void bn_finalize_kernel(double* __rest
                                                                   float* running_var, float momentum, float eps,
                                                                   float* scale, float* shift, float* save_mean,
                                                                   float* save_invstd, long long rep) {
-  __shared__ double red[kFinWaves * 48], tot[48];
-  const int c0 = blockIdx.x * 16;
-  slot_sums16<3>(acc, bn_fwd_slots(acc), C, c0, red, tot);
+  __shared__ double red[kFinThreads], tot[kFinCB * 3];
+  const int c0 = blockIdx.x * kFinCB;
+  slot_sums<3>(acc, bn_fwd_slots(acc), C, c0, red, tot);
   const int c = c0 + (int)threadIdx.x;
-  if (threadIdx.x >= 16 || c >= C) return;
+  if (threadIdx.x >= kFinCB || c >= C) return;
   const double S = tot[threadIdx.x * 3], Q = tot[threadIdx.x * 3 + 1], R = tot[threadIdx.x * 3 + 2];
   const double n = (double)rows;
   const double mean = S / n;
@@ -269,14 +270,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
   }
 }
 
-// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2 of channels [c0, c0 + 16) from the slots
-// of workspace acc (slot_sums16; every thread of the block calls it)
-__device__ __forceinline__ void bn_bwd_finalize16(double* __restrict__ acc, int C, int c0, double inv_rows,
-                                                  float* dgamma, float* dbeta, float* k1, float* k2) {
-  __shared__ double red[kFinWaves * 32], tot[32];
-  slot_sums16<2>(acc, bn_bwd_slots(acc, C), C, c0, red, tot);
+// dgamma/dbeta (accumulated into the gradient if non-null) and k1,k2 of channels [c0, c0 + kFinCB) from the
+// slots of workspace acc (slot_sums; every thread of the block calls it)
+__device__ __forceinline__ void bn_bwd_finalize_cb(double* __restrict__ acc, int C, int c0, double inv_rows,
+                                                   float* dgamma, float* dbeta, float* k1, float* k2) {
+  __shared__ double red[kFinThreads], tot[kFinCB * 2];
+  slot_sums<2>(acc, bn_bwd_slots(acc, C), C, c0, red, tot);
   const int c = c0 + (int)threadIdx.x;
-  if (threadIdx.x >= 16 || c >= C) return;
+  if (threadIdx.x >= kFinCB || c >= C) return;
   const double a = tot[threadIdx.x * 2], b = tot[threadIdx.x * 2 + 1];
   if (dbeta) dbeta[c] += (float)a;
   if (dgamma) dgamma[c] += (float)b;
@@ -284,23 +285,23 @@ __device__ __forceinline__ void bn_bwd_finalize16(double* __restrict__ acc, int 
   k2[c] = (float)(b * inv_rows);
 }
 
-// launch: kFinThreads threads per 16 channels
+// launch: kFinThreads threads per kFinCB channels
 __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize_kernel(double* __restrict__ acc, int C, double inv_rows,
                                                                       float* dgamma, float* dbeta, float* k1, float* k2) {
-  bn_bwd_finalize16(acc, C, blockIdx.x * 16, inv_rows, dgamma, dbeta, k1, k2);
+  bn_bwd_finalize_cb(acc, C, blockIdx.x * kFinCB, inv_rows, dgamma, dbeta, k1, k2);
 }
 
-// both BNs of a first block in one launch: blocks [0, G) the first BN's 16-channel groups, [G, 2G) the second's
+// both BNs of a first block in one launch: blocks [0, G) the first BN's channel groups, [G, 2G) the second's
 __global__ __launch_bounds__(kFinThreads) void bn_bwd_finalize2_kernel(double* __restrict__ acc, double* __restrict__ acc2,
                                                                        int C, double inv_rows, float* dgamma,
                                                                        float* dbeta, float* k1, float* k2,
                                                                        float* dgamma2, float* dbeta2, float* k1b,
                                                                        float* k2b) {
-  const int G = (C + 15) / 16;
+  const int G = (C + kFinCB - 1) / kFinCB;
   if ((int)blockIdx.x < G)
-    bn_bwd_finalize16(acc, C, blockIdx.x * 16, inv_rows, dgamma, dbeta, k1, k2);
+    bn_bwd_finalize_cb(acc, C, blockIdx.x * kFinCB, inv_rows, dgamma, dbeta, k1, k2);
   else
-    bn_bwd_finalize16(acc2, C, (blockIdx.x - G) * 16, inv_rows, dgamma2, dbeta2, k1b, k2b);
+    bn_bwd_finalize_cb(acc2, C, (blockIdx.x - G) * kFinCB, inv_rows, dgamma2, dbeta2, k1b, k2b);
 }
 
 // g_c = gamma*invstd*(g' - k1 - xhat*k2); optionally also writes g' (masked grad) to gmask_out.
@@ -727,7 +728,7 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
   hipStream_t st = (hipStream_t)stream;
   if (diag_skip(1, st)) return AVT_OK;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, rows, C, gamma,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }
@@ -742,7 +743,7 @@ extern "C" int avt_bn_finalize_rep(double* acc, long long rows, long long rep, i
                                    void* stream) {
   AVT_REQUIRE(acc && gamma && beta && scale && shift, "bn_finalize_rep: null pointer");
   AVT_REQUIRE(rows > 0 && C > 0 && rep >= 1, "bn_finalize_rep: empty input");
-  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, (hipStream_t)stream, acc, rows, C, gamma,
+  if (!diag_skip(1, (hipStream_t)stream)) hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, (hipStream_t)stream, acc, rows, C, gamma,
                      beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, rep);
   return check_launch("bn_finalize_rep");
 }
@@ -831,7 +832,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.C = C;
   if (t2) {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
-    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + 15) / 16)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + kFinCB - 1) / kFinCB)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
     p.mean2 = t2->mean;
@@ -843,7 +844,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
     hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
-    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
+    if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   }
@@ -869,7 +870,7 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
                        rows, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, (const bf16_t*)y,
@@ -892,7 +893,7 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)gm, nullptr,
@@ -914,7 +915,7 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16_t*)g, nullptr, scale,
@@ -959,7 +960,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
                        (long long)N * P * Q, C, st);
-  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 15) / 16), dim3(kFinThreads), 0, st, acc, C,
+  if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * ((H + 1) / 2)), dim3(kStemBwdThreads), (size_t)6 * Q * C,
                      st, (const bf16_t*)gy,

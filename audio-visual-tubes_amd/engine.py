@@ -290,14 +290,14 @@ class AVEngine:
         if self.concurrent and enabled and self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)
 
-    def _interleave(self, side_gen, main_gen):
+    def _interleave(self, side_gen, main_gen, phase: str = "BWD"):
         """Issue two launch generators (Trunk.*_iter) alternately, side_gen's launches on the side
         stream, main_gen's on the current one, forked before and joined after; returns both values.
         (Measured at B=32: the two-stream step 4.03 ms vs 5.26 ms on one stream.  The issue order
         does not matter to a HIP graph replay -- same-box A/B of interleaved vs branch-after-branch
         issue: equal -- and cross-stream edges that keep the branches in lockstep cost 9-24 %.)
         Not concurrent: side_gen then main_gen on the current stream."""
-        if not self.concurrent:
+        if not self.concurrent or os.environ.get("AVT_DEBUG_SERIAL_" + phase):  # (diagnostic: one phase serial)
             return drive(side_gen), drive(main_gen)
         side = self._side_stream()
         main = torch.cuda.current_stream()
@@ -449,7 +449,7 @@ class AVEngine:
             return out
 
         # audio trunk (side stream) || vision trunk (current stream), launches interleaved
-        (a, tape_a, an, amax, anorm), (v, tape_i) = self._interleave(audio_branch(), vision_branch())
+        (a, tape_a, an, amax, anorm), (v, tape_i) = self._interleave(audio_branch(), vision_branch(), "FWD")
         _, h, w, C = v.shape
         Pn = h * w
         L = B + (2 if self.neg else 1)
