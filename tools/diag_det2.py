@@ -27,7 +27,11 @@ if os.environ.get("DET_KEEP"):
             _keep.append(t)
             return t
         setattr(torch, _name, _wrap)
-img, aud = orc.make_image(6, 96).to(DEV), orc.make_spectrogram(6, 97, 110).to(DEV)
+_B = int(os.environ.get("DET_B", "6"))
+if os.environ.get("DET_FULL"):  # the bench's input sizes (224 x 224 frames, 257 x 300 spectrograms)
+    img, aud = orc.make_image(_B, 224).to(DEV), orc.make_spectrogram(_B, 257, 300).to(DEV)
+else:
+    img, aud = orc.make_image(_B, 96).to(DEV), orc.make_spectrogram(_B, 97, 110).to(DEV)
 runs = []
 NR = int(os.environ.get("DET_RUNS", "3"))
 for r in range(NR):
