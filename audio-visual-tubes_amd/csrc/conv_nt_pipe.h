@@ -38,9 +38,15 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // m0 carries the wave's LDS base.  It is not listed as clobbered: LLVM ignores clobbers of reserved
 // registers (with a warning per instantiation); the gfx950 code of these kernels has no other m0
 // use (no movrel/sendmsg; checked in the --save-temps assembly), so nothing live is overwritten.
+// The `s_nop 0` between the M0 write and the LDS-DMA is the required wait state (an SALU write of M0 ->
+// an LDS-DMA reading it; hipcc pads nothing inside an asm string).  Without it an LDS-DMA could take the
+// PREVIOUS M0 -- land on the previous instruction's LDS slot -- on some waves of some launches: run-to-run
+// differences of a few launches in hundreds (the small-tile halo dgrad at 32 clips,
+// test_small_grid_conv_repeatable / tools/diag_rep.py), which no tolerance check of the results can see.
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
   const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff), "s"(rs)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff),
+               "s"(rs)
                : "memory");
 }
 
