@@ -1,6 +1,7 @@
+# Determinism checks after a kernel change, then the full GPU suite + smoke (one box session).
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 env REP_FRESH=w python -u tools/diag_rep.py 32 14 14 512 512 60 > gpurun_out/rep1.log 2>&1 &&
 timeout -k 10 300 env REP_FRESH=w python -u tools/diag_rep.py 32 17 19 256 256 60 > gpurun_out/rep2.log 2>&1 &&
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 300 --timeout-method thread -m gpu -k "repeatable or determin" > gpurun_out/det_tests.log 2>&1 &&
-timeout -k 10 500 env DET_B=32 DET_FULL=1 DET_RUNS=3 python -u tools/diag_det2.py > gpurun_out/det2_b32.log 2>&1
+timeout -k 10 500 env DET_B=32 DET_FULL=1 DET_RUNS=3 python -u tools/diag_det2.py > gpurun_out/det2_b32.log 2>&1 &&
+bash tools/gpu_check.sh tests
