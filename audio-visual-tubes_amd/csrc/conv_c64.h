@@ -181,7 +181,7 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
         wait_vmcnt<0>();    // this half landed
       else
         wait_vmcnt<SPW>();  // ... (the previous tile's stores may be in flight)
-      __builtin_amdgcn_s_barrier();  // every wave's part landed; every wave is done with the other half-buffer
+      ring_barrier();  // every wave's part landed; every wave is done with the other half-buffer
       if (half == 0)
         issue_half(tile, 1);
       else

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
           wait_vmcnt<W0 + 3 * AP>();
         else
           wait_vmcnt<W0 + 4 * AP>();
-        if (!HALO_DBG(4)) __builtin_amdgcn_s_barrier();
+        if (!HALO_DBG(4)) ring_barrier();
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
         auto load_frags = [&](int ks, int buf) {
 #pragma unroll

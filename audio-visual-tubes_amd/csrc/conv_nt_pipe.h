@@ -28,6 +28,18 @@ constexpr unsigned kOOB = 0x80000000u;  // beyond any activation buffer: the loa
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+// The ring's barrier.  Every wave's LDS reads of the stage it is done with must have RETURNED before any
+// wave passes the barrier and DMAs the next tile into that stage.  s_barrier is no memory fence to the
+// compiler: it sinks a step's last MFMA below the barrier and with it the lgkmcnt wait for that MFMA's
+// fragment read (seen in the gfx950 assembly: `s_waitcnt lgkmcnt(1); s_barrier; ... lgkmcnt(3); mfma`), so
+// the read was still in flight while the other waves' DMA rewrote its stage -- rarely late enough to lose,
+// which showed as run-to-run differences (a few launches in hundreds of the small-tile halo kernels;
+// test_small_grid_conv_repeatable, tools/diag_rep.py).  The explicit lgkmcnt(0) retires them first.
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 // Issued as inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: the compiler treats every
 // LDS read after a builtin LDS-DMA as possibly aliasing it and inserts `s_waitcnt vmcnt(0)` in
 // front of the fragment reads, which drains ALL in-flight tiles each k-step and collapses the
@@ -287,7 +299,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
   };
   for (int kt = 0; kt < nkt; ++kt) {
     wait_vmcnt<(NST - 2) * LPT>();  // tile kt has landed (NST-2 younger tiles may be in flight)
-    __builtin_amdgcn_s_barrier();
+    ring_barrier();
     const char* As = smem + (kt % NST) * STAGE;
     const char* Bs = As + BM * RB;
     load_frags(As, Bs, 0, 0);

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
   if ((STAG & 2) && wtot >= (NW * KG) / 2) __builtin_amdgcn_s_setprio(1);
   for (int k = 0; k < nkt; ++k) {
     wait_vmcnt<(NST - 2) * LPT>();
-    __builtin_amdgcn_s_barrier();
+    ring_barrier();
     const char* As = smem + (k % NST) * STAGE;
     const char* Bs = As + A_BYTES;
     load_frags(As, Bs, 0, 0);

@@ -185,7 +185,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 
   for (int k = 0; k < nk; ++k) {
     wait_vmcnt<(NST - 2) * LPT>();
-    __builtin_amdgcn_s_barrier();
+    ring_barrier();
     const char* As = smem + (k % NST) * STAGE;
     const char* Ps = As + A_BYTES;
     // patch row (tap centre) of this lane's 4 fragment pixels: k = 16 ks + tr_row + 4 rr
