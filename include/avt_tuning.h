@@ -18,7 +18,7 @@ extern "C" {
  * (the first implementation, kept for A/B measurement; env AVT_CONV_VARIANT sets the default) */
 int avt_set_conv_variant(int variant);
 /* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) and nst64 (64 x 128
- * small-batch tile) in 2..5 (3 or more: one block per CU); all settings give bitwise-identical results (A/B knob) */
+ * small-batch tile) in 2..5 (one block per CU from nst128 = 3 / nst64 = 4 on); all settings give bitwise-identical results (A/B knob) */
 int avt_set_halo_stages(int nst128, int nst64);
 /* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
  * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
