@@ -228,3 +228,16 @@ def test_flatstore_mirror_and_deepcopy_rebind():
     with torch.no_grad():
         twin._flat.flat.zero_()
     assert dict(m.named_parameters())["imgnet.layer1.0.conv1.weight"].abs().sum() > 0
+
+
+@pytest.mark.parametrize("knob", ["AVT_DIAG_SKIP", "AVT_HALO_DBG"])
+def test_bench_refuses_wrong_results_knobs(knob):
+    """bench.py exits non-zero, before touching a GPU, when a wrong-results timing diagnostic is set."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, **{knob: "1"})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "1", "--warmup", "0"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "refusing" in (r.stderr + r.stdout) and knob in (r.stderr + r.stdout)
