@@ -574,6 +574,12 @@ static bool halo8_pick(const GemmNTParams& p) {
   if (p.IC >= 512) return true;
   return (long)((p.M + 255) / 256) * (p.Ng / 128) <= num_cus();
 }
+// weight-ring stages of the 8-wave 256 x 128 halo tile (A/B knob AVT_HALO8_NST: 3 default, or 4 -- the tile runs
+// one block per CU either way, so a fourth stage is one more weight tile in flight for free LDS)
+static int halo8_nst() {
+  static const int v = getenv("AVT_HALO8_NST") ? atoi(getenv("AVT_HALO8_NST")) : 3;
+  return v;
+}
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
 static int c64_enabled() {
   if (g_c64 < 0) {
@@ -1083,8 +1089,12 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     // gather on layer3/4 (W <= 19: +2..16 %); the 8-wave 256-row forms a patch of the wider layer1/2
     // images needs (1 block per CU) lose to it (-1..-20 %), so those keep the tap-gather kernel
     if (p.Ng % 128 == 0 && (g_halo == 2 || 128 + 2 * p.OW + 2 > 168 || halo8_pick(p))) {
-      if (256 + 2 * p.OW + 2 <= 336)
-        launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
+      if (256 + 2 * p.OW + 2 <= 336) {
+        if (halo8_nst() == 4)
+          launch_halo<MODE, 4, 2, 2, 2, 4, 336>(p, st);  // 4-stage weight ring: 150 KB of LDS, still 1 block/CU
+        else
+          launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
+      }
       else
         launch_halo<MODE, 4, 2, 2, 2, 2>(p, st);  // W <= 79: 2 weight stages to fit the 416-row patches
     }
