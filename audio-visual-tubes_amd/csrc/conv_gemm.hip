@@ -580,6 +580,13 @@ static int halo8_nst() {
   static const int v = getenv("AVT_HALO8_NST") ? atoi(getenv("AVT_HALO8_NST")) : 3;
   return v;
 }
+// wave layout of the 256 x 128 halo tile (A/B knob AVT_HALO8_FORM): 0 = 8 waves of 64 x 64 (TM = TN = 2: every
+// fragment read feeds two MFMAs, 1 KB of LDS reads per MFMA), 1 = 4 waves of 128 x 64 (TM = 4, TN = 2: 0.75 KB per
+// MFMA, one wave per SIMD with the whole register file)
+static int halo8_form() {
+  static const int v = getenv("AVT_HALO8_FORM") ? atoi(getenv("AVT_HALO8_FORM")) : 0;
+  return v;
+}
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
 static int c64_enabled() {
   if (g_c64 < 0) {
@@ -1090,7 +1097,9 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     // images needs (1 block per CU) lose to it (-1..-20 %), so those keep the tap-gather kernel
     if (p.Ng % 128 == 0 && (g_halo == 2 || 128 + 2 * p.OW + 2 > 168 || halo8_pick(p))) {
       if (256 + 2 * p.OW + 2 <= 336) {
-        if (halo8_nst() == 4)
+        if (halo8_form() == 1)
+          launch_halo<MODE, 2, 2, 4, 2, 3, 336>(p, st);  // same tile on 4 waves of 128 x 64 (0.75 KB LDS per MFMA)
+        else if (halo8_nst() == 4)
           launch_halo<MODE, 4, 2, 2, 2, 4, 336>(p, st);  // 4-stage weight ring: 150 KB of LDS, still 1 block/CU
         else
           launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
