@@ -52,6 +52,8 @@ SIGNATURES = {
     "avt_set_halo": (_I, [_I]),
     "avt_set_halo8": (_I, [_I]),
     "avt_set_halo_mf16": (_I, [_I]),
+    "avt_set_halo8_nst": (_I, [_I]),
+    "avt_set_halo8_form": (_I, [_I]),
     "avt_set_halo_stagger": (_I, [_I]),
     "avt_set_wgrad_stagger": (_I, [_I]),
     "avt_set_halo_stages": (_I, [_I, _I]),

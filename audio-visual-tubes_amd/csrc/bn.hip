@@ -44,11 +44,15 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
 constexpr int kFinWaves = 16, kFinThreads = kFinWaves * 64, kFinCB = 4;
 template <int W>
 __device__ __forceinline__ void slot_sums(const double* __restrict__ acc, const double* __restrict__ slots, int C,
-                                          int c0, double* red, double* tot) {
+                                          int c0, long long rows, double* red, double* tot) {
   constexpr int E = kFinCB * W, SPI = 64 / E, STEP = kFinWaves * SPI;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int so = lane / E, e = lane - so * E;
-  const int n = (int)acc[0] + (int)acc[1];
+  // the header's slot count, bounded by the workspace's capacity: a producer that skipped its header (or a
+  // workspace handed over uninitialised) gives NaN statistics, never reads beyond the slots
+  const double hn = acc[0] + acc[1];
+  const bool bad = !(hn >= 0.0 && hn <= (double)bn_slot_cap(rows));
+  const int n = bad ? 0 : (int)hn;
   double s = 0.0;
   if (so < SPI && c0 + e / W < C) {
     const double* base = slots + (size_t)c0 * W + e;
@@ -71,7 +75,7 @@ __device__ __forceinline__ void slot_sums(const double* __restrict__ acc, const 
     for (int ww = 0; ww < kFinWaves; ++ww)
 #pragma unroll
       for (int o = 0; o < SPI; ++o) t += red[ww * 64 + o * E + threadIdx.x];
-    tot[threadIdx.x] = t;
+    tot[threadIdx.x] = bad ? __builtin_nan("") : t;
   }
   __syncthreads();
 }
@@ -84,7 +88,7 @@ __global__ __launch_bounds__(kFinThreads) void bn_finalize_kernel(double* __rest
                                                                   float* save_invstd, long long rep) {
   __shared__ double red[kFinThreads], tot[kFinCB * 3];
   const int c0 = blockIdx.x * kFinCB;
-  slot_sums<3>(acc, bn_fwd_slots(acc), C, c0, red, tot);
+  slot_sums<3>(acc, bn_fwd_slots(acc), C, c0, rows, red, tot);
   const int c = c0 + (int)threadIdx.x;
   if (threadIdx.x >= kFinCB || c >= C) return;
   const double S = tot[threadIdx.x * 3], Q = tot[threadIdx.x * 3 + 1], R = tot[threadIdx.x * 3 + 2];
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16_t* __rest
 __device__ __forceinline__ void bn_bwd_finalize_cb(double* __restrict__ acc, int C, int c0, double inv_rows,
                                                    float* dgamma, float* dbeta, float* k1, float* k2) {
   __shared__ double red[kFinThreads], tot[kFinCB * 2];
-  slot_sums<2>(acc, bn_bwd_slots(acc, C), C, c0, red, tot);
+  slot_sums<2>(acc, bn_bwd_slots(acc, C), C, c0, __double2ll_rn(1.0 / inv_rows), red, tot);
   const int c = c0 + (int)threadIdx.x;
   if (threadIdx.x >= kFinCB || c >= C) return;
   const double a = tot[threadIdx.x * 2], b = tot[threadIdx.x * 2 + 1];
@@ -646,17 +650,20 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
   u32x4 sv[kStage];
   const u32x4* sg = reinterpret_cast<const u32x4*>(gy + ((size_t)n * P + p) * Q * C);
   const u32x4* si = reinterpret_cast<const u32x4*>(idx + ((size_t)n * P + p) * Q * C);
+  // rounds of kStage loads per thread (one round up to W = 168 at C = 64; wider rows take more, up to the LDS bound)
+  for (int t0 = 0; t0 < nst; t0 += kStage * kStemBwdThreads) {
 #pragma unroll
-  for (int j = 0; j < kStage; ++j) {
-    const int t = threadIdx.x + kStemBwdThreads * j;
-    if (t < nst) sv[j] = t < nrows * ng ? sg[t] : si[t - nrows * ng];  // consecutive pooled rows are contiguous
-  }
+    for (int j = 0; j < kStage; ++j) {
+      const int t = t0 + threadIdx.x + kStemBwdThreads * j;
+      if (t < nst) sv[j] = t < nrows * ng ? sg[t] : si[t - nrows * ng];  // consecutive pooled rows are contiguous
+    }
 #pragma unroll
-  for (int j = 0; j < kStage; ++j) {
-    const int t = threadIdx.x + kStemBwdThreads * j;
-    if (t < nst) {
-      char* dst = t < nrows * ng ? lds + (size_t)t * 16 : lds + 2 * rowg + (size_t)(t - nrows * ng) * 16;
-      *reinterpret_cast<u32x4*>(dst) = sv[j];
+    for (int j = 0; j < kStage; ++j) {
+      const int t = t0 + threadIdx.x + kStemBwdThreads * j;
+      if (t < nst) {
+        char* dst = t < nrows * ng ? lds + (size_t)t * 16 : lds + 2 * rowg + (size_t)(t - nrows * ng) * 16;
+        *reinterpret_cast<u32x4*>(dst) = sv[j];
+      }
     }
   }
   __syncthreads();
@@ -948,8 +955,7 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   AVT_REQUIRE(gy && idx && carg && c && scale && shift && mean && invstd && gamma && gc && workspace,
               "stem_maxpool_bn_relu_bwd: null pointer");
   AVT_REQUIRE(C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0, "stem_maxpool_bn_relu_bwd: C=%d unsupported", C);
-  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)2 * W * (C / 8) <= 6 * kStemBwdThreads &&
-                  (long long)((W + 1) / 2 + 1) * C * 6 / 16 <= 4 * kStemBwdThreads,
+  AVT_REQUIRE((long long)((W + 1) / 2 + 1) * C * 6 <= kStemLdsBytes && (long long)2 * W * (C / 8) <= 6 * kStemBwdThreads,
               "stem_maxpool_bn_relu_bwd: W=%d C=%d too wide", W, C);
   AVT_REQUIRE(N > 0 && H > 0 && W > 0, "stem_maxpool_bn_relu_bwd: empty input");
   AVT_REQUIRE(((uintptr_t)workspace & 7) == 0, "stem_maxpool_bn_relu_bwd: workspace must be 8-byte aligned");

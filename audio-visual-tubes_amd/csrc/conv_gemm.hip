@@ -14,48 +14,7 @@
 
 namespace avt {
 
-// ------------------------------------------------------------------------------------------------
-// NT kernel (fwd / dgrad)
-// ------------------------------------------------------------------------------------------------
-enum { MODE_FWD = 0, MODE_DGRAD = 1 };
-
-struct GemmNTParams {
-  const bf16_t* act;   // gather source: x [N][IH][IW][IC] (fwd) or dy [N][IH][IW][IC] (dgrad)
-  const bf16_t* wmat;  // [Ng][Kg] bf16, K contiguous
-  bf16_t* out;         // [M][Ng] bf16
-  const bf16_t* add;   // optional [M][Ng] bf16 added to the result (may alias out)
-  double* stats;       // optional BN accumulator (avt_common.h): per row tile t the fp32 results'
-                       // (sum_t, M2_t about the tile mean, sum_t^2/n_t) are stored into slot t
-  int M, Ng, Kg;
-  int IH, IW, IC;      // source tensor geometry
-  int OH, OW;          // pixel grid of the GEMM rows
-  int IT, OT;          // temporal extent of source / rows (Conv3d, temporal stride 1; 1 for Conv2d)
-  int KT, pad_t;       // temporal taps and padding (Conv3d; 1 / 0 for Conv2d)
-  int R, S, stride, pad;
-  // dgrad only -- fused BatchNorm-backward epilogue (conv_epi.h), active when bx != nullptr: the
-  // result g (after `add`) is masked by the ReLU of the BN that produced the positions' activations,
-  // g' = g * [by > 0] (by given: the block output) or g * [fma(bx, scale, shift) > 0] (BasicBlock.bn1),
-  // stored as g', and that BN's backward reductions (sum g', sum g' * xhat), xhat = (bx - mean)*invstd,
-  // are stored into slot bslot_base (+ bacc's header[0] when bappend) + the block's row tile of bacc (avt_common.h;
-  // bslot_total: the slots of all launches of this call, 0 = this launch's row tiles); bx2/bst2/bacc2 optionally a second BN fed
-  // by the same g' (the downsample BN of a first block: bn2 and downsample.1 share the ReLU).
-  const bf16_t* bx;
-  const bf16_t* by;
-  const float* bst;    // [4][Ng]: scale, shift, mean, invstd
-  double* bacc;
-  const bf16_t* bx2;
-  const float* bst2;
-  double* bacc2;
-  int bskip00;         // host side: a stride-2 dgrad's class-(0,0) launch stores plain g (another
-                       // kernel -- the downsample dgrad -- adds to those pixels and applies the epilogue)
-  int bslot_base, bslot_total, bappend;
-  const unsigned char* amask;  // optional [M][Ng/8] bits: `add` enters masked, add * bit (an identity
-                               // block's residual gradient g * [out > 0], from avt_bn_apply_mask's bits)
-};
-
-__device__ __forceinline__ int swz64(int row, int chunk) {  // byte offset in a [rows][32 bf16] tile
-  return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
-}
+#include "conv_params.h"
 
 template <int MODE, int CVEC, int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
@@ -576,16 +535,18 @@ static bool halo8_pick(const GemmNTParams& p) {
 }
 // weight-ring stages of the 8-wave 256 x 128 halo tile (A/B knob AVT_HALO8_NST: 3 default, or 4 -- the tile runs
 // one block per CU either way, so a fourth stage is one more weight tile in flight for free LDS)
+static int g_halo8_nst = -1;  // -1: env AVT_HALO8_NST (default 3)
 static int halo8_nst() {
-  static const int v = getenv("AVT_HALO8_NST") ? atoi(getenv("AVT_HALO8_NST")) : 3;
-  return v;
+  if (g_halo8_nst < 0) g_halo8_nst = getenv("AVT_HALO8_NST") ? atoi(getenv("AVT_HALO8_NST")) : 3;
+  return g_halo8_nst;
 }
 // wave layout of the 256 x 128 halo tile (A/B knob AVT_HALO8_FORM): 0 = 8 waves of 64 x 64 (TM = TN = 2: every
 // fragment read feeds two MFMAs, 1 KB of LDS reads per MFMA), 1 = 4 waves of 128 x 64 (TM = 4, TN = 2: 0.75 KB per
 // MFMA, one wave per SIMD with the whole register file)
+static int g_halo8_form = -1;  // -1: env AVT_HALO8_FORM (default 0)
 static int halo8_form() {
-  static const int v = getenv("AVT_HALO8_FORM") ? atoi(getenv("AVT_HALO8_FORM")) : 0;
-  return v;
+  if (g_halo8_form < 0) g_halo8_form = getenv("AVT_HALO8_FORM") ? atoi(getenv("AVT_HALO8_FORM")) : 0;
+  return g_halo8_form;
 }
 static int g_c64 = -1;  // layer-1 (C = K = 64, 3x3/s1) fwd/dgrad on conv_c64_kernel: -1 = env AVT_C64 (default 1)
 static int c64_enabled() {
@@ -1194,6 +1155,18 @@ extern "C" int avt_set_halo_stagger(int mode) {
   return AVT_OK;
 }
 
+extern "C" int avt_set_halo8_nst(int nst) {
+  AVT_REQUIRE(nst == -1 || nst == 3 || nst == 4, "set_halo8_nst: -1, 3 or 4");
+  avt::g_halo8_nst = nst;  // -1: back to the environment default
+  return AVT_OK;
+}
+
+extern "C" int avt_set_halo8_form(int form) {
+  AVT_REQUIRE(form >= -1 && form <= 1, "set_halo8_form: -1, 0 or 1");
+  avt::g_halo8_form = form;  // -1: back to the environment default
+  return AVT_OK;
+}
+
 extern "C" int avt_set_halo_mf16(int on) {
   AVT_REQUIRE(on >= -1 && on <= 1, "set_halo_mf16: -1, 0 or 1");
   avt::g_halo_mf16 = on;  // -1: back to the environment default
@@ -1286,6 +1259,9 @@ static int conv2d_dgrad_impl(const void* dy, const void* wt, void* dx, const voi
   AVT_REQUIRE(epi == nullptr || epi->xc2 == nullptr || (epi->stats2 && epi->acc2),
               "conv2d_dgrad: second BN needs stats2 and acc2");
   AVT_REQUIRE(epi == nullptr || ((uintptr_t)epi->acc & 7) == 0, "conv2d_dgrad: acc must be 8-byte aligned");
+  // only the LDS-DMA kernels write the epilogue's slots and header; the register-staged gemm_nt_kernel ignores it
+  AVT_REQUIRE(epi == nullptr || conv_variant() == 1,
+              "conv2d_dgrad: the BatchNorm-backward epilogue needs the LDS-DMA kernels (avt_set_conv_variant(1))");
   AVT_REQUIRE(C % 64 == 0 && K % 32 == 0, "conv2d_dgrad: C=%d K=%d unsupported", C, K);
   AVT_REQUIRE(stride == 1 || stride == 2, "conv2d_dgrad: stride must be 1 or 2");
   AVT_REQUIRE(R * S <= 32, "conv2d_dgrad: at most 32 taps");

@@ -75,8 +75,9 @@ constexpr int halo_blocks_per_cu() {
 // MFMAs past the next barrier (into the segment where their partners read fragments and issue DMA; the
 // fragments stay in registers, the accumulation order is unchanged: bitwise the same results); bit 1 = those
 // waves run at s_setprio 1 in the main loop (item 4)
+// PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop)
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
-          bool MF16 = false, int STAG = 0>
+          bool MF16 = false, int STAG = 0, int PREF = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   static_assert(!(MF16 && SPLIT), "split-K runs the 32x32x16 form");
@@ -251,6 +252,93 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   constexpr int LASTB = (KS - 1) & 1;  // fragment buffer of a step's last k-step
   const bool late = (STAG & 1) && wid >= NW / 2;  // wave-uniform
   if ((STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if constexpr (PREF) {
+    // PREF: each step's barrier also publishes the NEXT step's weight tile (and, at a chunk's last tap, the whole
+    // next patch), so the next step's first k-step fragments are read during this step's last MFMAs and the
+    // MFMAs of a step start right at its barrier -- no LDS round trip between the barrier and the first MFMA.
+    // Stages: step s reads stage s % NSTB, step s+1's tile sits landed in the next one, the DMA issued at step s
+    // fills step s+NSTB-1's (the stage step s-1 read: every wave retired those reads at barrier s).  The DMA has
+    // NSTB-2 steps to land (one at NSTB 3).  Accumulation order: unchanged (bitwise the same results).
+    static_assert(NSTB >= 3 && STAG == 0 && (KS & 1) == 0, "PREF: a 3+ stage ring, no stagger, even k-steps");
+    // the step-0 wait and barrier (weights of steps 0 .. NSTB-2 and chunk 0's patch were issued above)
+    // (taps 1 .. NSTB-2 carry no patch piece: only their weight tiles may be outstanding)
+    wait_vmcnt<(NSTB - 2) * BR>();
+    ring_barrier();
+    // PREF + 1 fragment buffers; k-step kk = t * KS + ks of a chunk uses buffer kk % NB (36 k-steps per chunk:
+    // NB divides it, so the buffer is a compile-time constant)
+    constexpr int NB = PREF + 1;
+    static_assert((9 * KS) % NB == 0 && PREF <= KS, "PREF");
+    bf16x8 pa[NB][FM], pb[NB][FN];
+    auto frags = [&](const char* Ab, const char* Bs, int t, int ks, int buf) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        pa[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << (MF16 ? 6 : 5))));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) pb[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
+    };
+    auto mmab = [&](int buf) {
+      if (HALO_DBG(8)) return;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (MF16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[buf][i], pb[buf][j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[buf][i], pb[buf][j], acc[i][j], 0, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int kk = 0; kk < PREF; ++kk) frags(smem, smem + 2 * ABUF, 0, kk, kk);
+    for (int c = 0; c < nchunk; ++c) {
+      const char* Ab = smem + (c & 1) * ABUF;          // patch buffer of this chunk
+      const char* Abn = smem + ((c + 1) & 1) * ABUF;   // ... and of the next (its first k-steps' prefetch)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int stage = NSTB == 3 ? t % 3 : (c * 9 + t) % NSTB;
+        const int nstage = NSTB == 3 ? (t + 1) % 3 : (c * 9 + t + 1) % NSTB;
+        // wait: step s+1's weights have landed once only what was issued after them may be outstanding --
+        // step s+1's own patch piece (relaxed, as below) and the issues of steps s+2 .. s+NSTB-2
+        int pieces = ((t + 1) % 9 >= NSTB - 1) ? 1 : 0;
+#pragma unroll
+        for (int j = 2; j <= NSTB - 2; ++j) pieces += ((t + j) % 9 >= NSTB - 1) ? 1 : 0;
+        constexpr int W0 = (NSTB - 3) * BR;
+        if (pieces == 0)
+          wait_vmcnt<W0>();
+        else if (pieces == 1)
+          wait_vmcnt<W0 + AP>();
+        else if (pieces == 2)
+          wait_vmcnt<W0 + 2 * AP>();
+        else
+          wait_vmcnt<W0 + 3 * AP>();
+        ring_barrier();
+        const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
+        const char* Bn = smem + 2 * ABUF + nstage * BSTAGE;
+        const bool more = t < 8 || c + 1 < nchunk;  // a next step exists (wave-uniform)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int kk = t * KS + ks, tk = kk + PREF;  // k-step read now (PREF ahead), in this chunk's numbering
+          if (tk < 9 * KS) {
+            if (tk / KS == t)
+              frags(Ab, Bs, t, tk % KS, tk % NB);
+            else
+              frags(Ab, Bn, t + 1, tk % KS, tk % NB);
+          } else if (more) {
+            frags(Abn, Bn, 0, tk - 9 * KS, tk % NB);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          mmab(kk % NB);
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks == 0) {  // the stage step s-1 read (every wave passed barrier s)
+            const int tn = t + NSTB - 1 >= 9 ? t + NSTB - 1 - 9 : t + NSTB - 1;
+            const int cn = t + NSTB - 1 >= 9 ? c + 1 : c;
+            issue(cn, tn, (stage + NSTB - 1) % NSTB);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  } else
   for (int c = 0; c < nchunk; ++c) {
     const char* Ab = smem + (c & 1) * ABUF;  // patch buffer of this chunk
 #pragma unroll

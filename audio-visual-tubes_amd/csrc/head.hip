@@ -640,13 +640,14 @@ __global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, in
   if (i < n) p[i] = 0.f;
 }
 
-// out[i] (+)= sum over s = 0 .. splits-1 of part[s * n + i], in that order
+// out[r * ldc + c] (+)= sum over s = 0 .. splits-1 of part[s * n + r * N + c] (dense M x N partials), in that order
 __global__ __launch_bounds__(256) void sgemm_sum_splits_kernel(const float* __restrict__ part, int splits, long long n,
-                                                               float* __restrict__ out, int accum) {
+                                                               int N, long long ldc, float* __restrict__ out, int accum) {
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     float v = 0.f;
     for (int s = 0; s < splits; ++s) v += part[s * n + i];
-    out[i] = accum ? out[i] + v : v;
+    const long long r = i / N, o = r * ldc + (i - r * N);
+    out[o] = accum ? out[o] + v : v;
   }
 }
 
@@ -667,9 +668,9 @@ static void sgemm(int M, int N, int K, const TA* a, long long sam, long long sak
   if (splits > 1) {
     hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
                        kscale, ws, (long long)N, kps, 0);
-    const long long n = (long long)M * N;  // ldc == N here (the head's outputs are dense)
+    const long long n = (long long)M * N;  // the partials are dense M x N; the sum honours ldc
     hipLaunchKernelGGL(sgemm_sum_splits_kernel, dim3((unsigned)min(2048LL, (n + 255) / 256)), dim3(256), 0, st, ws,
-                       splits, n, c, accum);
+                       splits, n, N, ldc, c, accum);
   } else {
     hipLaunchKernelGGL((sgemm_kernel<TA, TB>), grid, dim3(256), 0, st, M, N, K, a, sam, sak, b, sbk, sbn, rowscale,
                        kscale, c, ldc, kps, accum);

@@ -37,6 +37,13 @@ int avt_set_halo8(int on);
 /* 1: the halo fwd/dgrad tiles run on v_mfma_f32_16x16x32_bf16 (2x2 per 32x32 block) instead of 32x32x16;
  * 0: 32x32x16; -1: the environment default (AVT_HALO_MF16) — an A/B knob (fp32 sums in another order) */
 int avt_set_halo_mf16(int on);
+/* weight-ring stages of the 8-wave 256x128 halo tile: 3 (default) or 4 (150 KB of LDS, still one block per
+ * CU); -1: the environment default (AVT_HALO8_NST) — an A/B knob (bitwise the same results) */
+int avt_set_halo8_nst(int nst);
+/* wave layout of the 256x128 halo tile: 0 (default) = 8 waves of 64x64, 1 = 4 waves of 128x64 (0.75 KB of
+ * LDS reads per MFMA, one wave per SIMD); -1: the environment default (AVT_HALO8_FORM) — an A/B knob
+ * (bitwise the same results) */
+int avt_set_halo8_form(int form);
 /* the 8-wave halo tiles' SIMD-partner stagger: bit 0 = waves 4-7 run each tap step's last k-step of MFMAs
  * after the next barrier (bitwise the same results), bit 1 = waves 4-7 at s_setprio 1 in the main loop;
  * -1: the environment default (AVT_HALO_STAG, 0) — an A/B knob */

@@ -35,14 +35,6 @@ def S():
 
 
 DEV = "cuda"
-_KEEP = []  # device copies passed straight into a call(): referenced until the test ends
-
-
-@pytest.fixture(autouse=True)
-def _release_kept():
-    yield
-    torch.cuda.synchronize()
-    _KEEP.clear()
 
 
 def D(t):
@@ -704,7 +696,7 @@ def test_bn_relu_bwd(shape):
     assert rel_err(outs[0][2], bt.grad) < 1e-3
 
 
-@pytest.mark.parametrize("shape", [(2, 12, 14, 64), (2, 129, 150, 64), (1, 7, 9, 64), (3, 112, 112, 64)])
+@pytest.mark.parametrize("shape", [(2, 12, 14, 64), (2, 129, 150, 64), (1, 7, 9, 64), (3, 112, 112, 64), (2, 9, 192, 64)])
 def test_stem_fused(shape):
     """Stem bn1 -> relu -> maxpool fused both ways (base_models.py:200-203).  fwd: bitwise equal to
     avt_bn_apply + avt_maxpool3s2_fwd, carg = c at the argmax; bwd: fp64 autograd reference."""
@@ -1114,3 +1106,92 @@ def test_small_grid_conv_repeatable(case):
         assert torch.equal(o[0], outs[0][0]), f"launch {i}: forward output differs"
         assert torch.equal(o[2], outs[0][2]), f"launch {i}: BN partial sums differ"
         assert torch.equal(o[1], outs[0][1]), f"launch {i}: dgrad differs"
+
+
+@pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (2, 33, 38, 128, 128, 3, 1, 1)])
+def test_halo8_form_and_ring_bitwise_equal(case):
+    """The 8-wave 256 x 128 halo tile's A/B knobs (avt_set_halo8_form: 4 waves of 128 x 64; avt_set_halo8_nst:
+    a 4-stage weight ring) change the wave layout and the DMA depth, not the k order of any output: conv
+    outputs, plain dgrads, BN-epilogue dgrads (mask + slot sums) and the forward BN slots are bitwise equal."""
+    N, H, W, C, K, R, st, pad = case
+    x = _rand_act(N, H, W, C, 71).relu().to(DEV)
+    g = torch.Generator().manual_seed(72)
+    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
+    wf, wt = pack(w, C, R * R * C)
+    dy = _rand_act(N, H, W, K, 73).to(DEV)
+    xc, stats = _rand_act(N, H, W, C, 74).to(DEV), _bn_stats_rand(C, 75).to(DEV)
+    from avt_amd._lib import DgradBnEpi
+
+    call("avt_set_halo8", 1)
+    outs = []
+    try:
+        for form, nst in ((0, 3), (1, 3), (0, 4)):
+            call("avt_set_halo8_form", form)
+            call("avt_set_halo8_nst", nst)
+            y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
+            acc = fwd_acc(N * H * W, K)
+            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
+            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
+            ws = bwd_ws(N * H * W, C)
+            e = DgradBnEpi()
+            e.xc, e.stats, e.acc = P(xc).value, P(stats).value, ws.data_ptr()
+            dxe = torch.empty_like(dx)
+            call("avt_conv2d_dgrad_bn", P(dy), P(wt), P(dxe), None, N, H, W, C, K, R, R, st, pad, ctypes.byref(e), S())
+            torch.cuda.synchronize()
+            outs.append((y.view(torch.int16).clone(), dx.view(torch.int16).clone(), dxe.view(torch.int16).clone(),
+                         acc_sums(acc, K, 3), acc_sums(ws, C, 2, bwd=True)))
+    finally:
+        call("avt_set_halo8_form", -1)
+        call("avt_set_halo8_nst", -1)
+        call("avt_set_halo8", -1)
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b)
+    with pytest.raises(RuntimeError):
+        call("avt_set_halo8_nst", 5)
+
+
+def test_dgrad_bn_epilogue_needs_lds_dma_kernels():
+    """The register-staged conv variant (avt_set_conv_variant(0)) has no BN-backward epilogue: a dgrad that asks
+    for one is refused instead of leaving the accumulator's header and slots unwritten."""
+    N, H, W, C, K = 2, 9, 11, 64, 64
+    dy = _rand_act(N, H, W, K, 81).to(DEV)
+    w = (torch.randn(K, 3, 3, C, generator=torch.Generator().manual_seed(82)) * 0.05).float().to(DEV)
+    _, wt = pack(w, C, 9 * C)
+    xc, stats = _rand_act(N, H, W, C, 83).to(DEV), _bn_stats_rand(C, 84).to(DEV)
+    ws = bwd_ws(N * H * W, C)
+    from avt_amd._lib import DgradBnEpi
+
+    e = DgradBnEpi()
+    e.xc, e.stats, e.acc = P(xc).value, P(stats).value, ws.data_ptr()
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    call("avt_set_conv_variant", 0)
+    try:
+        with pytest.raises(RuntimeError, match="epilogue"):
+            call("avt_conv2d_dgrad_bn", P(dy), P(wt), P(dx), None, N, H, W, C, K, 3, 3, 1, 1, ctypes.byref(e), S())
+    finally:
+        call("avt_set_conv_variant", 1)
+
+
+@pytest.mark.parametrize("header", [float("nan"), -1.0, 1e9])
+def test_bn_finalize_rejects_bad_slot_header(header):
+    """A statistics accumulator whose header was never written (garbage slot count) gives NaN statistics
+    from avt_bn_finalize / avt_bn_bwd_premasked -- no reads beyond the workspace's slots."""
+    rows, C = 300, 64
+    acc = fwd_acc(rows, C)
+    acc[0], acc[1] = header, 0.0
+    gamma, beta = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    stats = torch.empty(4, C, device=DEV)
+    call("avt_bn_finalize", P(acc), rows, C, P(gamma), P(beta), None, None, ctypes.c_float(0.1),
+         ctypes.c_float(1e-5), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
+    ws = bwd_ws(rows, C)
+    ws.view(torch.float64)[0], ws.view(torch.float64)[1] = header, 0.0
+    g, xc = _rand_act(1, rows, 1, C, 85).to(DEV), _rand_act(1, rows, 1, C, 86).to(DEV)
+    dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    gc = torch.empty_like(g)
+    call("avt_bn_bwd_premasked", P(g), P(xc), P(stats[2]), P(stats[3]), P(gamma), P(dgamma), P(dbeta), P(gc),
+         P(ws), rows, C, S())
+    torch.cuda.synchronize()
+    assert torch.isnan(stats[2]).all() and torch.isnan(stats[3]).all()
+    assert torch.isnan(dbeta).all() and torch.isnan(dgamma).all()
