@@ -50,6 +50,24 @@ __device__ __forceinline__ void bn_write_header(double* acc, int nslots, int app
 }
 __device__ __forceinline__ int bn_slot_base(const double* acc, int append) { return append ? (int)acc[0] : 0; }
 
+// exact floor(n / d) for 32-bit n by a multiply-high and a shift (Granlund-Montgomery)
+struct MagicDiv {  // exact floor(n / d) for 32-bit n (Granlund-Montgomery)
+  unsigned m, l;
+};
+
+static inline MagicDiv make_magic(unsigned d) {
+  unsigned l = 0;
+  while ((1ull << l) < d) ++l;
+  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return MagicDiv{(unsigned)m, l};
+}
+
+__device__ __forceinline__ unsigned magic_div(unsigned n, MagicDiv md) {
+  if (md.l == 0) return n;  // d == 1
+  const unsigned t = __umulhi(md.m, n);
+  return (t + ((n - t) >> 1)) >> (md.l - 1);
+}
+
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 

@@ -75,7 +75,9 @@ constexpr int halo_blocks_per_cu() {
 // MFMAs past the next barrier (into the segment where their partners read fragments and issue DMA; the
 // fragments stay in registers, the accumulation order is unchanged: bitwise the same results); bit 1 = those
 // waves run at s_setprio 1 in the main loop (item 4)
-// PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop)
+// PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop).  Bench-only
+// (tools/halo_bench.hip, profiles/r5_halo_bench_pref.txt): +1..6 % on the layer4 shapes with a 4-stage ring, -3..5 %
+// on layer2; libavt launches PREF = 0
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
           bool MF16 = false, int STAG = 0, int PREF = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(

@@ -34,7 +34,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // fragment read (seen in the gfx950 assembly: `s_waitcnt lgkmcnt(1); s_barrier; ... lgkmcnt(3); mfma`), so
 // the read was still in flight while the other waves' DMA rewrote its stage -- rarely late enough to lose,
 // which showed as run-to-run differences (a few launches in hundreds of the small-tile halo kernels;
-// test_small_grid_conv_repeatable, tools/diag_rep.py).  The explicit lgkmcnt(0) retires them first.
+// test_small_grid_conv_repeatable, tools/diag.py rep).  The explicit lgkmcnt(0) retires them first.
 __device__ __forceinline__ void ring_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -54,7 +54,7 @@ __device__ __forceinline__ void ring_barrier() {
 // an LDS-DMA reading it; hipcc pads nothing inside an asm string).  Without it an LDS-DMA could take the
 // PREVIOUS M0 -- land on the previous instruction's LDS slot -- on some waves of some launches: run-to-run
 // differences of a few launches in hundreds (the small-tile halo dgrad at 32 clips,
-// test_small_grid_conv_repeatable / tools/diag_rep.py), which no tolerance check of the results can see.
+// test_small_grid_conv_repeatable / tools/diag.py rep), which no tolerance check of the results can see.
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
   const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff),

@@ -12,22 +12,7 @@
 // divisions.  NST-stage ring, NST-1 tiles in flight, split-K over blockIdx.y, fp32 atomics.
 #pragma once
 
-struct MagicDiv {  // exact floor(n / d) for 32-bit n (Granlund-Montgomery)
-  unsigned m, l;
-};
-
-static inline MagicDiv make_magic(unsigned d) {
-  unsigned l = 0;
-  while ((1ull << l) < d) ++l;
-  const unsigned long long m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
-  return MagicDiv{(unsigned)m, l};
-}
-
-__device__ __forceinline__ unsigned magic_div(unsigned n, MagicDiv md) {
-  if (md.l == 0) return n;  // d == 1
-  const unsigned t = __umulhi(md.m, n);
-  return (t + ((n - t) >> 1)) >> (md.l - 1);
-}
+// (MagicDiv, make_magic, magic_div: avt_common.h)
 
 struct GemmTNPipeParams {
   GemmTNParams p;

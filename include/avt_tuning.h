@@ -42,7 +42,7 @@ int avt_set_halo_mf16(int on);
 int avt_set_halo8_nst(int nst);
 /* wave layout of the 256x128 halo tile: 0 (default) = 8 waves of 64x64, 1 = 4 waves of 128x64 (0.75 KB of
  * LDS reads per MFMA, one wave per SIMD); -1: the environment default (AVT_HALO8_FORM) — an A/B knob
- * (bitwise the same results) */
+ * (bitwise the same outputs; the BN statistics summed over another wave partition) */
 int avt_set_halo8_form(int form);
 /* the 8-wave halo tiles' SIMD-partner stagger: bit 0 = waves 4-7 run each tap step's last k-step of MFMAs
  * after the next barrier (bitwise the same results), bit 1 = waves 4-7 at s_setprio 1 in the main loop;

@@ -38,6 +38,16 @@ def import_reference():
     return ref_model
 
 
+SAMPLE = 256  # strided gradient sample per parameter (direction checks of every parameter)
+
+
+def grad_sample(g: torch.Tensor) -> np.ndarray:
+    """SAMPLE values of a gradient at a fixed stride over the whole tensor (all of it when smaller)."""
+    f = g.detach().flatten()
+    stride = max(1, f.numel() // SAMPLE)
+    return f[::stride][:SAMPLE].double().numpy()
+
+
 def checksum(t: torch.Tensor) -> np.ndarray:
     t = t.detach().double().flatten()
     return np.array([t.sum().item(), (t * t).sum().item(), t[: min(16, t.numel())].sum().item()])
@@ -140,9 +150,17 @@ def make_fixture(ref_model, name, batch, img_size, freq, frames, seed_w=0):
         out["delta_slice_f64/" + n] = (r64["after"][n] - r64["before"][n]).flatten()[:64].numpy()
     for n in BUF_SLICES:
         out["buf_f64/" + n] = r64["bufs"][n][:16].numpy()
-    dev = deviation(run_reference_bf16_trunks(ref_model, sd, image, audio), r64, names, batch)
+    rb = run_reference_bf16_trunks(ref_model, sd, image, audio)
+    dev = deviation(rb, r64, names, batch)
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
+    # per-parameter gradient samples of the fp64 truth and of the bf16-autocast yardstick (tests bound EVERY
+    # parameter by its own yardstick: tests/gradcheck.py)
+    for n in names:
+        out["grad_sample_f64/" + n] = grad_sample(r64["grads"][n])
+        out["bf16ref_sample/" + n] = grad_sample(rb["grads"][n])
+    for n in SLICE_PARAMS:
+        out["bf16ref_slice/" + n] = rb["grads"][n].flatten()[:64].double().numpy()
     print(f"[{name}] bf16-trunk reference deviation: " + ", ".join(
         f"{k}={np.max(v) if k != 'slice_cos' else np.min(v):.3e}" for k, v in dev.items()))
     out["image_checksum"] = checksum(image)

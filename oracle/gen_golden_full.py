@@ -28,23 +28,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import avenet_oracle as orc  # noqa: E402
 import tube_oracle as tor  # noqa: E402
-from gen_golden import OUT, SLICE_PARAMS, checksum, import_reference  # noqa: E402
+from gen_golden import OUT, SAMPLE, SLICE_PARAMS, checksum, grad_sample, import_reference  # noqa: E402,F401
 
 # BNs whose running statistics are stored in full: both stems' bn1 (the largest reductions), a
 # layer1 BN, a stride-2 downsample BN and the last BN of each trunk
 FULL_BUFS = [p + s for p in ("imgnet.", "audnet.") for s in
              ("bn1", "layer1.0.bn1", "layer2.0.downsample.1", "layer4.1.bn2")]
 TUBE_BUFS = ["audnet.bn1", "audnet.layer1.0.bn1", "audnet.layer4.1.bn2", "vidnet.bn1", "vidnet.layer4.1.bn2"]
-
-
-SAMPLE = 256  # strided gradient sample per parameter (direction checks of every parameter)
-
-
-def grad_sample(g: torch.Tensor) -> np.ndarray:
-    """SAMPLE values of a gradient at a fixed stride over the whole tensor (all of it when smaller)."""
-    f = g.detach().flatten()
-    stride = max(1, f.numel() // SAMPLE)
-    return f[::stride][:SAMPLE].double().numpy()
 
 
 def _peak_gb():

@@ -1,0 +1,78 @@
+"""Per-parameter gradient checks against the reference's golden vectors, shared by the GPU parity tests: every
+parameter gradient is bounded by ITS OWN yardstick -- the reference's trunks run under bf16 autocast on the same
+inputs (oracle/gen_golden.py, oracle/gen_golden_full.py store a strided 256-value sample of every fp64 and
+bf16-autocast gradient)."""
+import numpy as np
+
+
+def _cos(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(a @ b / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-300))
+
+
+def _sample(t, n=256):
+    """gen_golden_full.grad_sample of a gradient in the reference's (OIHW-contiguous) element order."""
+    f = t.detach().contiguous().flatten()
+    return f[::max(1, f.numel() // n)][:n].double().cpu().numpy()
+
+
+def check_grads(g, grads, tag=""):
+    """Every parameter's gradient against the fp64 reference, each bounded by ITS OWN yardstick -- the
+    reference's trunks under bf16 autocast at the same size (stored by gen_golden_full.py).  On a
+    256-value strided sample s of each tensor (all of it when smaller; the first 64 values of the
+    SLICE_PARAMS as a second sample):
+      * error vector   e = |s - s64| / |s64|  <=  max(5e-2, 3 e_ref);
+      * direction      cos(s, s64)  >=  min(0.999, 1 - 3 (1 - cos_ref));
+      * norm           | |g| / |g64| - 1 |  <=  max(5e-2, 3 dref, e_ref) -- dref the yardstick's own norm
+        deviation, and e_ref its error-vector size: by the triangle inequality a gradient that far from
+        the truth may differ in norm by that much.  This matters for the channel-sum gradients (BN
+        affine parameters, the audio stem) whose bf16 error is as large as the value itself: there the
+        yardstick's cosine is 0.5-0.9 and one run's norm deviation is a noisy statistic;
+      * the median norm deviation over all parameters within 3x the yardstick's median.
+    grads: name -> gradient shaped like the Parameter (OIHW)."""
+    from gen_golden import SLICE_PARAMS
+
+    names = [str(n) for n in g["param_names"]]
+    gn = np.array([grads[n].norm().item() for n in names])
+    rel = np.abs(gn - g["grad_norm_f64"]) / g["grad_norm_f64"]
+    dref = g["bf16ref_dev/gradnorm_rel"]
+    samples = {}
+    for n in names:
+        if "grad_sample_f64/" + n in g:
+            samples[(n, "sample")] = (_sample(grads[n]), g["grad_sample_f64/" + n], g["bf16ref_sample/" + n])
+    for n in SLICE_PARAMS:
+        if "bf16ref_slice/" + n in g and n in grads:
+            samples[(n, "slice")] = (grads[n].detach().contiguous().flatten()[:64].double().cpu().numpy(),
+                                     g["grad_slice_f64/" + n], g["bf16ref_slice/" + n])
+    assert samples, "fixture without gradient samples (regenerate with oracle/gen_golden_full.py)"
+
+    def err(v, ref):
+        return float(np.linalg.norm(v - ref) / max(np.linalg.norm(ref), 1e-300))
+
+    bad, worst_c, worst_e = [], (None, 1.0), (None, 0.0)
+    e_ref_of = {}
+    for (n, kind), (v, ref, vb) in samples.items():
+        e, er, c, cr = err(v, ref), err(vb, ref), _cos(v, ref), _cos(vb, ref)
+        if kind == "sample":
+            e_ref_of[n] = er
+        if c < worst_c[1]:
+            worst_c = (f"{n} ({kind}, yardstick {cr:.4f})", c)
+        if e / max(5e-2, 3 * er) > worst_e[1]:
+            worst_e = (f"{n} ({kind}: {e:.4f} vs yardstick {er:.4f})", e / max(5e-2, 3 * er))
+        if e > max(5e-2, 3 * er):
+            bad.append((n, kind, "error", round(e, 4), round(er, 4)))
+        if c < min(0.999, 1 - 3 * (1 - cr)):
+            bad.append((n, kind, "cosine", round(c, 5), round(cr, 5)))
+    tol = np.array([max(5e-2, 3 * d, e_ref_of.get(n, 0.0)) for n, d in zip(names, dref)])
+    for i, n in enumerate(names):
+        if rel[i] > tol[i]:
+            bad.append((n, "norm", round(float(rel[i]), 4), round(float(tol[i]), 4)))
+    worst = names[int((rel / tol).argmax())]
+    print(f"{tag} grad-norm rel err max {rel.max():.3e} ({worst}, {float((rel / tol).max()):.2f} of its bound) "
+          f"median {np.median(rel):.3e} (bf16 reference max {dref.max():.3e} median {np.median(dref):.3e})")
+    print(f"{tag} {len(samples)} sampled gradients: lowest cosine {worst_c[1]:.5f} {worst_c[0]}; largest error "
+          f"vector {worst_e[1]:.2f} of its bound: {worst_e[0]}")
+    for b in bad:
+        print(f"{tag} OUT OF BOUND {b}")
+    assert not bad, (tag, bad)
+    assert np.median(rel) <= 3 * np.median(dref) + 1e-3, (tag, np.median(rel))

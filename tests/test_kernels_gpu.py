@@ -1112,7 +1112,8 @@ def test_small_grid_conv_repeatable(case):
 def test_halo8_form_and_ring_bitwise_equal(case):
     """The 8-wave 256 x 128 halo tile's A/B knobs (avt_set_halo8_form: 4 waves of 128 x 64; avt_set_halo8_nst:
     a 4-stage weight ring) change the wave layout and the DMA depth, not the k order of any output: conv
-    outputs, plain dgrads, BN-epilogue dgrads (mask + slot sums) and the forward BN slots are bitwise equal."""
+    outputs, plain dgrads and BN-epilogue dgrads are bitwise equal; the BN slot sums are bitwise equal under the
+    4-stage ring and equal to rounding under the 4-wave form (its reduction partition differs)."""
     N, H, W, C, K, R, st, pad = case
     x = _rand_act(N, H, W, C, 71).relu().to(DEV)
     g = torch.Generator().manual_seed(72)
@@ -1145,9 +1146,16 @@ def test_halo8_form_and_ring_bitwise_equal(case):
         call("avt_set_halo8_form", -1)
         call("avt_set_halo8_nst", -1)
         call("avt_set_halo8", -1)
-    for o in outs[1:]:
-        for a, b in zip(o, outs[0]):
+    # outputs and dgrads bitwise; the 4-wave form sums the statistics over its own wave/thread partition (another
+    # fp32 order): its slots to rounding, the 4-stage ring's bitwise
+    for form, o in zip((1, 0), outs[1:]):
+        for a, b in zip(o[:3], outs[0][:3]):
             assert torch.equal(a, b)
+        for a, b in zip(o[3:], outs[0][3:]):
+            if form:
+                np.testing.assert_allclose(a.numpy(), b.numpy(), rtol=1e-5, atol=1e-6 * b.abs().max().item())
+            else:
+                assert torch.equal(a, b)
     with pytest.raises(RuntimeError):
         call("avt_set_halo8_nst", 5)
 

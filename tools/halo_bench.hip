@@ -2,7 +2,7 @@
 // libavt so a variant compiles in seconds: per trunk shape and mode, the variants run on the same inputs, their
 // outputs and BN slots are compared bit for bit with the first (baseline) variant, and each is timed with HIP
 // events over alternating rounds of back-to-back launches (random data: the clock depends on the operands).
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Iaudio-visual-tubes_amd/csrc tools/halo_bench.hip
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Iaudio-visual-tubes_amd/csrc -Itools tools/halo_bench.hip
 //        -o tools/halo_bench        run: tools/halo_bench [B] [rounds] [launches]
 #include "avt_common.h"
 
@@ -14,6 +14,7 @@ namespace avt {
 #include "conv_epi.h"
 #include "conv_nt_pipe.h"
 #include "conv_halo.h"
+#include "halo_pk.h"
 void set_error(const char* fmt, ...) { (void)fmt; }
 int check_launch(const char*) { return hipGetLastError() == hipSuccess ? AVT_OK : AVT_EHIP; }
 }  // namespace avt
@@ -51,17 +52,43 @@ void launch_v(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t s
                      dim3(WM * WN * 64), 0, st, p, ha);
 }
 
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PK, int DBG = 0>
+void launch_pk(const GemmNTParams& p, const HaloArgs& ha0, int grid, hipStream_t st) {
+  HaloPkArgs ha;
+  static_cast<HaloArgs&>(ha) = ha0;
+  ha.div_hw = make_magic((unsigned)(ha0.W * ha0.H));
+  ha.div_w = make_magic((unsigned)ha0.W);
+  ha.pk = PK;
+  static int ncu = 0;
+  if (!ncu) {
+    hipDeviceProp_t pr;
+    (void)hipGetDeviceProperties(&pr, 0);
+    ncu = getenv("HB_G") ? atoi(getenv("HB_G")) : pr.multiProcessorCount;
+    fprintf(stderr, "multiProcessorCount %d, G %d\n", pr.multiProcessorCount, ncu);
+  }
+  int G = ncu;  // one block per CU
+  if (PK == 1 && grid < G) G = grid;
+  hipLaunchKernelGGL((conv_halo_pk_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, PK, DBG>), dim3(G), dim3(WM * WN * 64), 0, st, p, ha);
+}
+
 struct Variant {
   std::string name;
   Launcher fn[2];  // fwd, dgrad
   int BM, BN, PRMAX;
+  int pk;          // stream-K: needs >= nc units per block
 };
 
 template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF>
 Variant make(const char* name) {
   return Variant{name,
                  {launch_v<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PREF>, launch_v<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PREF>},
-                 WM * TM * 32, WN * TN * 32, PRMAX};
+                 WM * TM * 32, WN * TN * 32, PRMAX, 0};
+}
+template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PK, int DBG = 0>
+Variant make_pk(const char* name) {
+  return Variant{name,
+                 {launch_pk<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PK, DBG>, launch_pk<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PK, DBG>},
+                 WM * TM * 32, WN * TN * 32, PRMAX, PK};
 }
 
 int main(int argc, char** argv) {
@@ -78,14 +105,20 @@ int main(int argc, char** argv) {
   if (argc > 4 && !strcmp(argv[4], "sweep"))  // one / two rounds of 256 tiles (16 x 16 images), K = 18 / 36 / 72 steps
     shapes = {{"s128x1", 256, 16, 16, 128, 128}, {"s256x1", 256, 16, 16, 256, 128}, {"s512x1", 256, 16, 16, 512, 128},
               {"s128x2", 512, 16, 16, 128, 128}, {"s256x2", 512, 16, 16, 256, 128}, {"s512x2", 512, 16, 16, 512, 128}};
-  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make<4, 2, 2, 2, 4, 336, 1>("p1n4"),
-                               make<4, 2, 2, 2, 3, 336, 2>("p2n3"), make<4, 2, 2, 2, 4, 336, 2>("p2n4")};
+  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make_pk<4, 2, 2, 2, 3, 336, 1>("pk1"),
+                               make_pk<4, 2, 2, 2, 3, 336, 2>("pk2"), make_pk<4, 2, 2, 2, 3, 336, 1, 1>("pk1ns"),
+                               make_pk<4, 2, 2, 2, 3, 336, 1, 3>("pk1nss")};
   hipStream_t st;
   HIPCHECK(hipStreamCreate(&st));
   hipEvent_t e0, e1;
   HIPCHECK(hipEventCreate(&e0));
   HIPCHECK(hipEventCreate(&e1));
   int bad = 0;
+  float* part;
+  int* cnt;
+  HIPCHECK(hipMalloc(&part, (size_t)256 * 256 * 128 * 4));
+  HIPCHECK(hipMalloc(&cnt, 256 * 4));
+  HIPCHECK(hipMemset(cnt, 0, 256 * 4));
   for (const Shape& s : shapes) {
     for (int mode = 0; mode < 2; ++mode) {
       const int IC = mode == 0 ? s.C : s.K, Ng = mode == 0 ? s.K : s.C;
@@ -108,6 +141,7 @@ int main(int argc, char** argv) {
       p.IT = p.OT = p.KT = 1; p.R = p.S = 3; p.stride = 1; p.pad = 1;
       HaloArgs ha{};
       ha.ksplit = 1; ha.cps = IC / 64;
+      ha.part = part; ha.cnt = cnt;
       ha.dbg = argc > 5 ? atoi(argv[5]) : 0;  // -DAVT_DIAG build only (conv_halo.h HALO_DBG; wrong results)
       ha.act_bytes = (unsigned)(act_n * 2);
       ha.w_bytes = (unsigned)(w_n * 2);
@@ -118,12 +152,17 @@ int main(int argc, char** argv) {
           const int dy = mode == 0 ? r - 1 : 1 - r, dx = mode == 0 ? c - 1 : 1 - c;
           ha.tap_dy[t] = dy; ha.tap_dx[t] = dx; ha.tap_disp[t] = dy * s.W + dx; ha.tap_w[t] = t;
         }
+      auto fits = [&](const Variant& V) {
+        if (Ng % V.BN != 0 || V.BM + 2 * s.W + 2 > V.PRMAX) return false;
+        const long long tiles = (M + V.BM - 1) / V.BM * (Ng / V.BN);
+        return V.pk != 2 || tiles >= 256;  // stream-K: >= nc units per block
+      };
       std::vector<unsigned short> ref_out(out_n), got(out_n);
       std::vector<double> ref_st, got_st;
       std::vector<double> best(vars.size(), 1e30), sum(vars.size(), 0.0);
       for (size_t v = 0; v < vars.size(); ++v) {
         const Variant& V = vars[v];
-        if (Ng % V.BN != 0 || V.BM + 2 * s.W + 2 > V.PRMAX) { fprintf(stderr, "shape/variant mismatch\n"); return 2; }
+        if (!fits(V)) continue;  // the variant does not fit the shape
         const int grid = (int)((M + V.BM - 1) / V.BM) * (Ng / V.BN);
         HIPCHECK(hipMemsetAsync(out, 0xff, out_n * 2, st));
         V.fn[mode](p, ha, grid, st);
@@ -153,6 +192,7 @@ int main(int argc, char** argv) {
       for (int r = 0; r < rounds; ++r)
         for (size_t v = 0; v < vars.size(); ++v) {
           const Variant& V = vars[v];
+          if (!fits(V)) continue;
           const int grid = (int)((M + V.BM - 1) / V.BM) * (Ng / V.BN);
           for (int i = 0; i < 3; ++i) V.fn[mode](p, ha, grid, st);
           HIPCHECK(hipEventRecord(e0, st));
@@ -167,7 +207,8 @@ int main(int argc, char** argv) {
         }
       printf("%-5s %-5s M=%7lld N=%4d K=%5d |", s.name, mode ? "dgrad" : "fwd", M, Ng, 9 * IC);
       for (size_t v = 0; v < vars.size(); ++v)
-        printf("  %s %7.1f us %5.0f TF/s", vars[v].name.c_str(), sum[v] / rounds, flop / (sum[v] / rounds * 1e-6) / 1e12);
+        if (sum[v] > 0)
+          printf("  %s %7.1f us %5.0f TF/s", vars[v].name.c_str(), sum[v] / rounds, flop / (sum[v] / rounds * 1e-6) / 1e12);
       printf("\n");
       fflush(stdout);
       HIPCHECK(hipFree(act));
