@@ -51,11 +51,9 @@ SIGNATURES = {
     "avt_set_nt64_config": (_I, [_I]),
     "avt_set_halo": (_I, [_I]),
     "avt_set_halo8": (_I, [_I]),
-    "avt_set_halo_mf16": (_I, [_I]),
     "avt_set_halo8_nst": (_I, [_I]),
+    "avt_conv_stem_dgrad": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "avt_set_halo8_form": (_I, [_I]),
-    "avt_set_halo_stagger": (_I, [_I]),
-    "avt_set_wgrad_stagger": (_I, [_I]),
     "avt_set_halo_stages": (_I, [_I, _I]),
     "avt_set_c64": (_I, [_I]),
     "avt_set_s2_dgrad_one": (_I, [_I]),

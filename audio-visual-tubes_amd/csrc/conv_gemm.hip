@@ -478,8 +478,6 @@ static int g_wgrad_slab_max = 1 << 30;
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
-static int g_wgrad_stag = -1;  // the 8-wave TN wgrad blocks' SIMD-partner stagger (conv_tn_pipe.h): -1 = env AVT_WGRAD_STAG
-static int g_halo_stag = -1;   // ... and the 8-wave halo tiles' (conv_halo.h): -1 = env AVT_HALO_STAG
 static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
                                    // measured 230-320 TFLOP/s vs 450-820 for the tap-gather kernel, see
@@ -515,12 +513,6 @@ static int halo_nst() {
 static int halo_small_nst() {
   if (g_halo_small_nst < 0) g_halo_small_nst = getenv("AVT_HALO_SMALL_NST") ? atoi(getenv("AVT_HALO_SMALL_NST")) : 3;
   return g_halo_small_nst;
-}
-// halo fwd/dgrad on v_mfma_f32_16x16x32_bf16 tiles (conv_halo.h MF16) instead of 32x32x16: -1 = env AVT_HALO_MF16
-static int g_halo_mf16 = -1;
-static int halo_mf16() {
-  if (g_halo_mf16 < 0) g_halo_mf16 = getenv("AVT_HALO_MF16") ? atoi(getenv("AVT_HALO_MF16")) : 0;
-  return g_halo_mf16;
 }
 // the 8-wave 256 x 128 halo tile (one block per CU) in place of the 128 x 128 one where measured faster
 // (tools/conv_bench.py --halo 1,2; B=128): layer4 (K = 4608: V +5..7 %, A +6..7 %; B=32 A +9 %) and GEMMs
@@ -837,22 +829,10 @@ static bool use_small_tile(const GemmNTParams& p, int BN) {
   return blocks128 < (long long)g_small_tile_waves * num_cus();
 }
 
-static int halo_stag() {
-  if (g_halo_stag < 0) g_halo_stag = getenv("AVT_HALO_STAG") ? atoi(getenv("AVT_HALO_STAG")) : 0;
-  return g_halo_stag;
-}
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI, bool MF16>
-static void launch_halo_stag(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t st) {
-  const dim3 blk(WM * WN * 64);
-  if constexpr (WM * WN == 8) {
-    switch (halo_stag() & 3) {
-      case 1: hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI, false, MF16, 1>), dim3(grid), blk, 0, st, p, ha); return;
-      case 2: hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI, false, MF16, 2>), dim3(grid), blk, 0, st, p, ha); return;
-      case 3: hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI, false, MF16, 3>), dim3(grid), blk, 0, st, p, ha); return;
-      default: break;
-    }
-  }
-  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI, false, MF16>), dim3(grid), blk, 0, st, p, ha);
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI>
+static void launch_halo_one(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI>), dim3(grid), dim3(WM * WN * 64), 0, st,
+                     p, ha);
 }
 
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR>
@@ -889,17 +869,10 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
     return;
   }
   if (grid <= 0) return;
-  const bool epi = MODE == MODE_DGRAD && p.bx != nullptr;
-  if (halo_mf16()) {
-    if (epi)
-      launch_halo_stag<MODE, WM, WN, TM, TN, NSTB, PRMAX, true, true>(p, ha, grid, st);
-    else
-      launch_halo_stag<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, true>(p, ha, grid, st);
-  } else if (epi) {
-    launch_halo_stag<MODE, WM, WN, TM, TN, NSTB, PRMAX, true, false>(p, ha, grid, st);
-  } else {
-    launch_halo_stag<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false>(p, ha, grid, st);
-  }
+  if (MODE == MODE_DGRAD && p.bx != nullptr)
+    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>(p, ha, grid, st);
+  else
+    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false>(p, ha, grid, st);
 }
 
 // the 4-wave 128 x 128 halo tile by weight-ring depth (avt_set_halo_stages / AVT_HALO_NST): 2 stages (80 KB
@@ -1143,18 +1116,6 @@ extern "C" int avt_conv2d_splitk_plan(int N, int H, int W, int C, int K, int R, 
   return AVT_OK;
 }
 
-extern "C" int avt_set_wgrad_stagger(int mode) {
-  AVT_REQUIRE(mode >= -1 && mode <= 3, "set_wgrad_stagger: -1 .. 3");
-  g_wgrad_stag = mode;
-  return AVT_OK;
-}
-
-extern "C" int avt_set_halo_stagger(int mode) {
-  AVT_REQUIRE(mode >= -1 && mode <= 3, "set_halo_stagger: -1 .. 3");
-  g_halo_stag = mode;  // -1: back to the environment default
-  return AVT_OK;
-}
-
 extern "C" int avt_set_halo8_nst(int nst) {
   AVT_REQUIRE(nst == -1 || nst == 3 || nst == 4, "set_halo8_nst: -1, 3 or 4");
   avt::g_halo8_nst = nst;  // -1: back to the environment default
@@ -1164,12 +1125,6 @@ extern "C" int avt_set_halo8_nst(int nst) {
 extern "C" int avt_set_halo8_form(int form) {
   AVT_REQUIRE(form >= -1 && form <= 1, "set_halo8_form: -1, 0 or 1");
   avt::g_halo8_form = form;  // -1: back to the environment default
-  return AVT_OK;
-}
-
-extern "C" int avt_set_halo_mf16(int on) {
-  AVT_REQUIRE(on >= -1 && on <= 1, "set_halo_mf16: -1, 0 or 1");
-  avt::g_halo_mf16 = on;  // -1: back to the environment default
   return AVT_OK;
 }
 
@@ -1478,19 +1433,9 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   return pl;
 }
 
-static int wgrad_stag() {
-  if (g_wgrad_stag < 0) g_wgrad_stag = getenv("AVT_WGRAD_STAG") ? atoi(getenv("AVT_WGRAD_STAG")) : 0;
-  return g_wgrad_stag;
-}
 template <int WM, int WN, int TM, int TN, int NST, int KG>
-static void launch_tn_stag(dim3 grid, const GemmTNPipeParams& pp, hipStream_t st) {
-  const dim3 blk(WM * WN * 64 * KG);
-  switch (wgrad_stag() & 3) {
-    case 1: hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG, 1>), grid, blk, 0, st, pp); return;
-    case 2: hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG, 2>), grid, blk, 0, st, pp); return;
-    case 3: hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG, 3>), grid, blk, 0, st, pp); return;
-    default: hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG>), grid, blk, 0, st, pp); return;
-  }
+static void launch_tn_one(dim3 grid, const GemmTNPipeParams& pp, hipStream_t st) {
+  hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG>), grid, dim3(WM * WN * 64 * KG), 0, st, pp);
 }
 
 template <int CVEC, int BM, int BN>
@@ -1511,12 +1456,12 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
       else if (pl.nst == 4)
         hipLaunchKernelGGL((conv_tn_pipe_kernel<4, 2, 2, 4, 4>), grid, dim3(512), 0, st, pp);
       else
-        launch_tn_stag<4, 2, 2, 4, 3, 1>(grid, pp, st);
+        launch_tn_one<4, 2, 2, 4, 3, 1>(grid, pp, st);
     } else if constexpr (BM == 256) {
-      launch_tn_stag<4, 2, 2, 2, 3, 1>(grid, pp, st);
+      launch_tn_one<4, 2, 2, 2, 3, 1>(grid, pp, st);
     } else {
       if (pl.kg == 2)
-        launch_tn_stag<2, 2, BM / 64, BN / 64, 4, 2>(grid, pp, st);
+        launch_tn_one<2, 2, BM / 64, BN / 64, 4, 2>(grid, pp, st);
       else if (pl.nst >= 8)
         hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 8>), grid, dim3(256), 0, st, pp);
       else if (pl.nst >= 6)

@@ -49,18 +49,13 @@ __device__ __forceinline__ f32x4 load_wt16(__amdgpu_buffer_rsrc_t rs, unsigned o
 }
 
 // LDS chunk swizzle of a 128-B row (8 16-B chunks): the 32x32x16 fragment reads (lanes 0-31 one chunk of 32
-// consecutive rows) are conflict-free with chunk ^ ((row >> 1) & 7); the 16x16x32 reads (a 16-lane bank
-// group = rows +0..3 and +12..15 of one chunk and rows +4..11 of the next) with chunk ^ (row & 6) -- for
-// ANY first row, which the tap shifts of the patch make arbitrary (exhaustive check over the 16 offsets)
-template <bool MF16>
-__device__ __forceinline__ int halo_swz(int row) {
-  return MF16 ? (row & 6) : ((row >> 1) & 7);
-}
+// consecutive rows) are conflict-free with chunk ^ ((row >> 1) & 7) -- for ANY first row, which the tap shifts of
+// the patch make arbitrary (exhaustive check over the 16 offsets)
+__device__ __forceinline__ int halo_swz(int row) { return (row >> 1) & 7; }
 
-// WM x WN waves, each TM x TN 32x32 output blocks: BM = WM*TM*32 rows, BN = WN*TN*32 columns.  MF16: each
-// 32x32 block as 2x2 v_mfma_f32_16x16x32_bf16 tiles instead of one v_mfma_f32_32x32x16_bf16 (same cycles
-// per FLOP, same LDS bytes per FLOP; the chip holds a higher clock under the 16x16 shape on random data,
-// MI355X_MICROARCH.md DVFS item 7).
+// WM x WN waves, each TM x TN 32x32 output blocks (v_mfma_f32_32x32x16_bf16): BM = WM*TM*32 rows, BN = WN*TN*32
+// columns.  (A 16x16x32 form and a SIMD-partner stagger of the 8-wave tiles were measured in rounds 3-4 and
+// removed in round 5: DESIGN.md section 6.)
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
 // EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
 // LDS of the main loop (two patch buffers + the weight ring): two blocks per CU when two fit in 160 KB
@@ -69,23 +64,16 @@ constexpr int halo_blocks_per_cu() {
   return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
-// STAG (8-wave tiles, two waves per SIMD running the same program between per-tap barriers, which keeps them
-// in lockstep -- both SIMD partners reach their MFMAs, their LDS reads and the barrier together;
-// MI355X_MICROARCH.md "Two waves per SIMD" item 9): bit 0 = waves NW/2.. defer each tap step's last k-step
-// MFMAs past the next barrier (into the segment where their partners read fragments and issue DMA; the
-// fragments stay in registers, the accumulation order is unchanged: bitwise the same results); bit 1 = those
-// waves run at s_setprio 1 in the main loop (item 4)
 // PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop).  Bench-only
 // (tools/halo_bench.hip, profiles/r5_halo_bench_pref.txt): +1..6 % on the layer4 shapes with a 4-stage ring, -3..5 %
 // on layer2; libavt launches PREF = 0
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
-          bool MF16 = false, int STAG = 0, int PREF = 0>
+          int PREF = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
-  static_assert(!(MF16 && SPLIT), "split-K runs the 32x32x16 form");
   // fragment geometry: FM x FN MFMA tiles of FR rows per wave, KS k-steps of KD per 64-channel tap
-  constexpr int FR = MF16 ? 16 : 32, FM = MF16 ? 2 * TM : TM, FN = MF16 ? 2 * TN : TN;
-  constexpr int KD = MF16 ? 32 : 16;
+  constexpr int FR = 32, FM = TM, FN = TN;
+  constexpr int KD = 16;
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   constexpr int BK = 64, RB = 128, RPI = 8;  // 64 channels = one 128-B row; 8 rows per 1 KiB DMA
@@ -138,18 +126,18 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     const int pr = q * RPI + lrow;
     const int pix = m0 - pre + pr;
     if (q >= PINSTR || pr >= PR || pix < 0 || pix >= p.M) return kOOB;
-    const int lc = pchunk ^ halo_swz<MF16>(pr);
+    const int lc = pchunk ^ halo_swz(pr);
     return (unsigned)(((long long)pix * p.IC + chunk_c * BK + lc * 8) * 2);
   };
   unsigned b_off[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int row = (wid * BR + i) * RPI + lrow;
-    const int lc = pchunk ^ halo_swz<MF16>(row);
+    const int lc = pchunk ^ halo_swz(row);
     b_off[i] = (unsigned)(((size_t)(n0 + row) * p.Kg + lc * 8) * 2);
   }
   // ---- fragment rows of this lane: rows wm*(BM/WM) + i*FR + (lane % FR); per row a 9-bit tap mask.  The
-  //      lane's k chunk within a k-step: fhalf (32x32x16: lanes 32-63 take k 8..15) or lane >> 4 (16x16x32) ----
+  //      lane's k chunk within a k-step: fhalf (lanes 32-63 take k 8..15) ----
   const int frow = lane & (FR - 1), fhalf = lane / FR;
   unsigned fmask[FM];
 #pragma unroll
@@ -174,7 +162,6 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   //      B: per (column block, k-step) offset in a ring stage.  With the tap loop unrolled the k loop is
   //      ds_read + MFMA (tap, stage and buffer are compile-time; a rolled (chunk, tap) loop spent ~11
   //      other instructions per MFMA) ----
-  // (MF16: the chunk is k-step * 4 + lane >> 4, so a k-step is an XOR of ks << 6)
   unsigned arow[9][FM];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -182,7 +169,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     for (int i = 0; i < FM; ++i) {
       const int pr = wm * (BM / WM) + i * FR + frow + pre + ha.tap_disp[t];
       const bool v = (fmask[i] >> t) & 1u;
-      arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((fhalf ^ halo_swz<MF16>(pr)) << 4));
+      arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((fhalf ^ halo_swz(pr)) << 4));
     }
   constexpr int KS = BK / KD;
   int boffs[FN][KS];
@@ -191,7 +178,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int row = wn * (BN / WN) + j * FR + frow;
-      boffs[j][ks] = row * RB + ((((MF16 ? 4 : 2) * ks + fhalf) ^ halo_swz<MF16>(row)) << 4);
+      boffs[j][ks] = row * RB + (((2 * ks + fhalf) ^ halo_swz(row)) << 4);
     }
 
   // ---- issue of step (chunk cn, tap tn): weight tile into ring stage (cn*9+tn) % NSTB, and for tn >=
@@ -220,11 +207,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 
   // accumulators: AV fp32 per lane per MFMA tile; element v of tile (i, j) is output row acc_row(i, v),
   // column wn*(BN/WN) + j*FR + frow
-  constexpr int AV = MF16 ? 4 : 16;
-  using acc_t = typename std::conditional<MF16, f32x4, f32x16>::type;
-  auto acc_row = [&](int i, int v) -> int {
-    return wm * (BM / WM) + i * FR + (MF16 ? fhalf * 4 + v : (v & 3) + 8 * (v >> 2) + 4 * fhalf);
-  };
+  constexpr int AV = 16;
+  using acc_t = f32x16;
+  auto acc_row = [&](int i, int v) -> int { return wm * (BM / WM) + i * FR + (v & 3) + 8 * (v >> 2) + 4 * fhalf; };
   acc_t acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -245,15 +230,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        if constexpr (MF16)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
-        else
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
       }
   };
-  constexpr int LASTB = (KS - 1) & 1;  // fragment buffer of a step's last k-step
-  const bool late = (STAG & 1) && wid >= NW / 2;  // wave-uniform
-  if ((STAG & 2) && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   if constexpr (PREF) {
     // PREF: each step's barrier also publishes the NEXT step's weight tile (and, at a chunk's last tap, the whole
     // next patch), so the next step's first k-step fragments are read during this step's last MFMAs and the
@@ -261,7 +240,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     // Stages: step s reads stage s % NSTB, step s+1's tile sits landed in the next one, the DMA issued at step s
     // fills step s+NSTB-1's (the stage step s-1 read: every wave retired those reads at barrier s).  The DMA has
     // NSTB-2 steps to land (one at NSTB 3).  Accumulation order: unchanged (bitwise the same results).
-    static_assert(NSTB >= 3 && STAG == 0 && (KS & 1) == 0, "PREF: a 3+ stage ring, no stagger, even k-steps");
+    static_assert(NSTB >= 3 && (KS & 1) == 0, "PREF: a 3+ stage ring, even k-steps");
     // the step-0 wait and barrier (weights of steps 0 .. NSTB-2 and chunk 0's patch were issued above)
     // (taps 1 .. NSTB-2 carry no patch piece: only their weight tiles may be outstanding)
     wait_vmcnt<(NSTB - 2) * BR>();
@@ -274,7 +253,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     auto frags = [&](const char* Ab, const char* Bs, int t, int ks, int buf) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        pa[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << (MF16 ? 6 : 5))));
+        pa[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
 #pragma unroll
       for (int j = 0; j < FN; ++j) pb[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
     };
@@ -284,10 +263,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          if constexpr (MF16)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[buf][i], pb[buf][j], acc[i][j], 0, 0, 0);
-          else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[buf][i], pb[buf][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[buf][i], pb[buf][j], acc[i][j], 0, 0, 0);
         }
     };
 #pragma unroll
@@ -376,7 +352,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         auto load_frags = [&](int ks, int buf) {
 #pragma unroll
           for (int i = 0; i < FM; ++i)
-            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << (MF16 ? 6 : 5))));
+            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
 #pragma unroll
           for (int j = 0; j < FN; ++j) bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
         };
@@ -387,29 +363,22 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
           const int stn = NSTB == 2 ? (stage ^ 1) : (stage + NSTB - 1) % NSTB;
           issue(cn, tn, stn);
         }
-        if (late && (t > 0 || c > 0)) {  // the previous step's deferred last k-step (its fragments in LASTB)
-          __builtin_amdgcn_sched_barrier(0);
-          mma(LASTB);
-          __builtin_amdgcn_sched_barrier(0);
-        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           if (ks + 1 < KS) {
             load_frags(ks + 1, (ks + 1) & 1);
             __builtin_amdgcn_sched_barrier(0);
           }
-          if (ks + 1 < KS || !late) mma(ks & 1);
+          mma(ks & 1);
           if (ks + 1 < KS) __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
   }
-  if (late) mma(LASTB);  // the last step's deferred k-step
-  if (STAG & 2) __builtin_amdgcn_s_setprio(0);
   wait_vmcnt<0>();
   __syncthreads();
 
-  if constexpr (SPLIT && !MF16) {
+  if constexpr (SPLIT) {
     // partial tile in register order: (wave, i, j, quarter) x 64 lanes x 16 B -- 1 KiB per instruction
     const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(ha.part + (size_t)tile * ha.ksplit * BM * BN), (short)0, (int)(ha.ksplit * BM * BN * 4), 0x00020000);

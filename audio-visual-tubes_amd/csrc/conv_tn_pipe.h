@@ -30,10 +30,7 @@ __device__ __forceinline__ int tn_swz(int row) {  // chunk XOR for a row of ROWB
 // KG = 2: two such wave groups per block split the block's k range in halves, each through its own LDS
 // ring, and meet in LDS at the end -- one partial tile per block instead of two (the split-K slab
 // traffic, which dominates the short-batch wgrads, halves at the same number of waves)
-// STAG (8-wave blocks: two waves per SIMD that barrier together every k-tile and so run in lockstep): as
-// conv_halo.h -- bit 0 = the second half of the waves runs each k-tile's last k-step of MFMAs after the next
-// barrier (same accumulation order: bitwise the same results), bit 1 = that half at s_setprio 1
-template <int WM, int WN, int TM, int TN, int NST, int KG = 1, int STAG = 0>
+template <int WM, int WN, int TM, int TN, int NST, int KG = 1>
 __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
   constexpr int NW = WM * WN;  // waves per group
   static_assert(KG == 1 || KG == 2, "one or two k groups");
@@ -210,8 +207,6 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
   };
-  const bool late = (STAG & 1) && wtot >= (NW * KG) / 2;  // wave-uniform
-  if ((STAG & 2) && wtot >= (NW * KG) / 2) __builtin_amdgcn_s_setprio(1);
   for (int k = 0; k < nkt; ++k) {
     wait_vmcnt<(NST - 2) * LPT>();
     ring_barrier();
@@ -219,20 +214,13 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
     const char* Bs = As + A_BYTES;
     load_frags(As, Bs, 0, 0);
     issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);
-    if (late && k > 0) {  // the previous k-tile's deferred second k-step (fragments in buffer 1)
-      __builtin_amdgcn_sched_barrier(0);
-      mma(1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     // step 1's fragments are read while step 0 multiplies
     load_frags(As, Bs, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (!late) mma(1);
+    mma(1);
   }
-  if (late && nkt > 0) mma(1);
-  if (STAG & 2) __builtin_amdgcn_s_setprio(0);
   wait_vmcnt<0>();
   if constexpr (KG > 1) {  // group 1's accumulators into group 0's, through the (now idle) rings
     __syncthreads();

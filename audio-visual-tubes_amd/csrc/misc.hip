@@ -323,6 +323,54 @@ __global__ __launch_bounds__(256) void copy16_kernel(const u32x4* __restrict__ s
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) dst[i] = src[i];
 }
 
+
+// ---- input gradient of the 7x7 / s2 / p3 stem conv ----
+// One thread per input pixel (n, h, w): the output positions (p, q) that read it are p = (h + 3 - r) / 2 for the
+// rows r of matching parity (<= 4 of the 7), likewise q; gx[c] = sum over those (r, s) and the 64 output channels
+// of gy[n][p][q][k] * w[k][r][s][c], in a fixed order.  The weights (64 x 49 x Cin fp32) sit in LDS tap-major
+// ([r][s][k][4]).  VALU work: an optional path (only when the trunk input requires grad), not the train step's.
+constexpr int kStemDgThreads = 256;
+__global__ __launch_bounds__(kStemDgThreads) void stem_dgrad_kernel(const bf16_t* __restrict__ gy,
+                                                                   const float* __restrict__ w, float* __restrict__ gx,
+                                                                   int N, int H, int W, int P, int Q, int Cin) {
+  __shared__ float ws[49 * 64 * 4];
+  for (int i = threadIdx.x; i < 49 * 64 * 4; i += kStemDgThreads) {
+    const int c = i & 3, k = (i >> 2) & 63, t = i >> 8;  // t = r * 7 + s
+    ws[i] = c < Cin ? w[((size_t)k * 49 + t) * Cin + c] : 0.f;
+  }
+  __syncthreads();
+  const long long pix = blockIdx.x * (long long)kStemDgThreads + threadIdx.x;
+  if (pix >= (long long)N * H * W) return;
+  const int n = (int)(pix / ((long long)H * W));
+  const int rem = (int)(pix - (long long)n * H * W);
+  const int h = rem / W, x = rem - h * W;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = (h + 3) & 1; r < 7; r += 2) {
+    const int p = (h + 3 - r) >> 1;
+    if (p < 0 || p >= P) continue;
+    for (int s = (x + 3) & 1; s < 7; s += 2) {
+      const int q = (x + 3 - s) >> 1;
+      if (q < 0 || q >= Q) continue;
+      const u32x4* row = reinterpret_cast<const u32x4*>(gy + (((size_t)n * P + p) * Q + q) * 64);
+      const float* wt = ws + (r * 7 + s) * 256;
+#pragma unroll 2
+      for (int k8 = 0; k8 < 8; ++k8) {
+        const u32x4 v = row[k8];
+        const unsigned* u = reinterpret_cast<const unsigned*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = bf2f((bf16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffff));
+          const float4 wk = *reinterpret_cast<const float4*>(wt + (k8 * 8 + e) * 4);
+          acc[0] += g * wk.x;
+          acc[1] += g * wk.y;
+          acc[2] += g * wk.z;
+          acc[3] += g * wk.w;
+        }
+      }
+    }
+  }
+  for (int c = 0; c < Cin; ++c) gx[(((size_t)n * Cin + c) * H + h) * W + x] = acc[c];
+}
 }  // namespace avt
 
 using namespace avt;
@@ -418,6 +466,18 @@ extern "C" int avt_pack_conv_weight(const float* w, int K, int R, int S, int C, 
 // descs: device array of n records {const float* w; void* fwd; void* dgrad; int K, RS, C, Cp, Kg, pad}
 // (48 bytes each, layout of PackDesc); two launches pack every conv weight of the model.
 extern "C" size_t avt_pack_desc_bytes(void) { return sizeof(PackDesc); }
+
+extern "C" int avt_conv_stem_dgrad(const void* gy, const float* w, float* gx, int N, int H, int W, int Cin,
+                                   void* stream) {
+  AVT_REQUIRE(gy && w && gx, "conv_stem_dgrad: null pointer");
+  AVT_REQUIRE(N > 0 && H > 0 && W > 0 && Cin >= 1 && Cin <= 4, "conv_stem_dgrad: N=%d H=%d W=%d Cin=%d", N, H, W, Cin);
+  const int P = (H + 6 - 7) / 2 + 1, Q = (W + 6 - 7) / 2 + 1;
+  const long long pix = (long long)N * H * W;
+  AVT_REQUIRE(pix < (1LL << 31) * (long long)kStemDgThreads, "conv_stem_dgrad: input too large");
+  hipLaunchKernelGGL(stem_dgrad_kernel, dim3((unsigned)((pix + kStemDgThreads - 1) / kStemDgThreads)),
+                     dim3(kStemDgThreads), 0, (hipStream_t)stream, (const bf16_t*)gy, w, gx, N, H, W, P, Q, Cin);
+  return check_launch("conv_stem_dgrad");
+}
 
 extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long max_elems, void* stream) {
   AVT_REQUIRE(descs && n > 0, "pack_conv_weights_batched: bad arguments");

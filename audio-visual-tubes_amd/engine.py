@@ -581,7 +581,7 @@ class AVEngine:
 class TrunkEngine(AVEngine):
     """One ResNet-18 trunk called on its own (``model.imgnet(x)`` / a standalone ``resnet18(modal=...)``,
     base_models.py:195-213): NCHW fp32 input -> layer4 map NCHW fp32, backward into the trunk's
-    parameter gradients (the stem's input gradient is not computed)."""
+    parameter gradients (and the input gradient through the 7x7 stem when asked: avt_conv_stem_dgrad)."""
 
     def __init__(self, flat: FlatStore, prefix: str, modal: str):
         self._prefix, self._modal = prefix, modal
@@ -612,10 +612,12 @@ class TrunkEngine(AVEngine):
         return out, tape
 
     def backward(self, tape, g_out: torch.Tensor, gflat: torch.Tensor):
-        """g_out [N,512,h,w] fp32 (any layout) -> parameter gradients accumulated into gflat."""
+        """g_out [N,512,h,w] fp32 (any layout) -> parameter gradients accumulated into gflat; returns the input
+        gradient [N,Cin,H,W] fp32 when tape["want_dx"] was set, else None."""
         g = g_out.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()  # layout plumbing
         self.store.grads = self.flat.grad_views(gflat)
         try:
             self.trunk.backward(tape, g, self.store, None)
         finally:
             self.store.grads = None
+        return tape.get("dx")

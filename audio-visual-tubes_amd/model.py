@@ -132,10 +132,10 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         eng, flat, names, params = self._engine_and_params()
-        if x.requires_grad and torch.is_grad_enabled():
-            raise NotImplementedError("avt: gradients w.r.t. the trunk input are not computed (the reference "
-                                      "feeds data tensors; the 7x7 stem's dgrad is not built)")
-        need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in params)
+        need_grad = torch.is_grad_enabled() and (x.requires_grad or (self.training and any(p.requires_grad for p in params)))
+        if need_grad and not self.training:
+            raise NotImplementedError("avt: gradients through an eval-mode trunk are not computed (train-mode "
+                                      "BatchNorm only)")
         if need_grad:
             return _TrunkFunction.apply(eng, names, x, *params)
         out, _ = eng.forward(x, self.training)
@@ -146,6 +146,7 @@ class _TrunkFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, names, x, *params):
         out, tape = engine.forward(x, True)
+        tape["want_dx"] = ctx.needs_input_grad[2]  # d(loss)/d(x) through the 7x7 stem (avt_conv_stem_dgrad)
         ctx.engine, ctx.tape, ctx.names = engine, tape, names
         ctx.set_materialize_grads(False)
         return out
@@ -158,10 +159,10 @@ class _TrunkFunction(torch.autograd.Function):
             raise RuntimeError("avt: second backward through a trunk forward")
         flat = ctx.engine.flat
         gflat = torch.zeros(flat.n_train, device=g.device, dtype=torch.float32)
-        ctx.engine.backward(ctx.tape, g, gflat)
+        gx = ctx.engine.backward(ctx.tape, g, gflat)
         ctx.tape = None
         views = flat.param_grad_views(gflat)
-        return (None, None, None) + tuple(views[n] for n in ctx.names)
+        return (None, None, gx) + tuple(views[n] for n in ctx.names)
 
 
 class HardWayArgs:

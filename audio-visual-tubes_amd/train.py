@@ -119,13 +119,6 @@ class HardWayTrainStep:
             pos = max(pos, hi)
         return out["loss"]
 
-    def _allreduce_bucket(self, tags, works: list):
-        """Issue the async all-reduce of the bucket(s) a backward boundary made final (one tag, or a
-        tuple of tags reached together); RCCL's stream waits for the current stream's work so far."""
-        for tag in ((tags,) if isinstance(tags, str) else tags):
-            lo, hi = self.buckets[tag]
-            works.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
-
     def step(self, *inputs: torch.Tensor) -> torch.Tensor:
         """step(image, audio).  Returns the local mean CE loss (device scalar, no host sync)."""
         if self._graph is not None or self._seg_graphs is not None:
@@ -145,11 +138,55 @@ class HardWayTrainStep:
             dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.pg)
             self.opt.step(self.grad, grad_scale=1.0 / self.world)
             return loss
-        works: list = []
-        loss = self._fwd_bwd(*inputs, on_boundary=lambda tags: self._allreduce_bucket(tags, works))
-        for w in works:  # the current stream waits for RCCL's (no host sync)
-            w.wait()
-        self.opt.step(self.grad, grad_scale=1.0 / self.world)
+        return self._fwd_bwd_dp(*inputs)
+
+    def _adam_stream(self):
+        if getattr(self, "_adam_side", None) is None:
+            self._adam_side = torch.cuda.Stream(device=self.grad.device)
+        return self._adam_side
+
+    def _dp_boundary(self, tags, pending: list):
+        """World > 1, at a backward boundary: the bucket(s) just made final go out as async all-reduces; an
+        upper-layer ("hi") bucket is then updated on the Adam side stream as soon as its collective completes --
+        while the next backward segment computes -- and a "lo" bucket is left for the end of the step."""
+        side = self._adam_stream()
+        for tag in ((tags,) if isinstance(tags, str) else tags):
+            lo, hi = self.buckets[tag]
+            work = dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            if tag.endswith("hi"):
+                side.wait_stream(torch.cuda.current_stream())  # Adam's prep (step counter) and the gradients
+                with torch.cuda.stream(side):
+                    work.wait()  # the side stream waits for RCCL's (no host sync)
+                    self.opt.apply(self.grad, lo, hi, grad_scale=1.0 / self.world)
+            else:
+                pending.append((lo, hi, work))
+
+    def _dp_finish(self, pending: list):
+        for lo, hi, work in pending:
+            work.wait()
+            self.opt.apply(self.grad, lo, hi, grad_scale=1.0 / self.world)
+        torch.cuda.current_stream().wait_stream(self._adam_stream())
+
+    def _fwd_bwd_dp(self, *inputs) -> torch.Tensor:
+        """World > 1 (overlap): forward with Adam's prep and the gradient zeroing on the vision branch (as at world
+        1), backward in two segments with each bucket's all-reduce issued at its boundary and its Adam update
+        applied as soon as that collective completes (_dp_boundary); the update of every parameter equals
+        opt.step(all-reduced gradient, 1/world)."""
+        def pre():
+            self.opt.prep()
+            self.grad.zero_()
+
+        image, audio = inputs
+        if type(self)._fwd_bwd is HardWayTrainStep._fwd_bwd and self.vision_pre:
+            out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0, vision_pre=pre)
+            pending: list = []
+            self.engine.backward(tape, out["dlogits"], self.grad, lambda tags: self._dp_boundary(tags, pending))
+            self._dp_finish(pending)
+            return out["loss"]
+        self.opt.prep()
+        pending = []
+        loss = self._fwd_bwd(*inputs, on_boundary=lambda tags: self._dp_boundary(tags, pending))
+        self._dp_finish(pending)
         return loss
 
     def capture(self, *inputs: torch.Tensor) -> None:
@@ -210,17 +247,27 @@ class HardWayTrainStep:
                     g2.capture_begin(pool=pool)
                     graphs.append(g2)
 
-            loss = self._fwd_bwd(*inputs, on_boundary=boundary)
+            # Adam's prep rides in the first segment (on the vision branch, as _fwd_bwd_dp); the per-bucket updates
+            # stay eager between the replays (_dp_boundary / _dp_finish), each behind its collective
+            if type(self)._fwd_bwd is HardWayTrainStep._fwd_bwd and self.vision_pre:
+                def pre():
+                    self.opt.prep()
+                    self.grad.zero_()
+
+                image, audio = inputs
+                out, tape = self.engine.forward(image, audio, training=True, with_ce=True, ce_scale=1.0,
+                                                vision_pre=pre)
+                self.engine.backward(tape, out["dlogits"], self.grad, boundary)
+                loss = out["loss"]
+            else:
+                self.opt.prep()
+                loss = self._fwd_bwd(*inputs, on_boundary=boundary)
             if not tags or last_tag not in ((tags[-1],) if isinstance(tags[-1], str) else tuple(tags[-1])):
                 raise RuntimeError("avt: backward did not reach its last gradient bucket")
-            g_opt = torch.cuda.CUDAGraph()
-            g_opt.capture_begin(pool=pool)
-            self.opt.step(self.grad, grad_scale=1.0 / self.world)
-            g_opt.capture_end()
         torch.cuda.current_stream().wait_stream(stream)
         torch.cuda.synchronize()
         self._static_loss = loss
-        self._seg_graphs, self._seg_tags, self._graph_opt = graphs, tags, g_opt
+        self._seg_graphs, self._seg_tags, self._graph_opt = graphs, tags, None
 
     def _replay(self, *inputs: torch.Tensor) -> torch.Tensor:
         if len(inputs) != len(self._static_in) or any(
@@ -233,13 +280,11 @@ class HardWayTrainStep:
                 s.copy_(x)
         if self._seg_graphs is not None:
             sync_buffers(self.flat.bflat, self.pg)
-            works: list = []
+            pending: list = []
             for g, tag in zip(self._seg_graphs, self._seg_tags):
                 g.replay()
-                self._allreduce_bucket(tag, works)  # overlaps the next segment's replay
-            for w in works:
-                w.wait()
-            self._graph_opt.replay()
+                self._dp_boundary(tag, pending)  # collectives + "hi" updates overlap the next segment's replay
+            self._dp_finish(pending)
         elif self._graph_opt is not None:
             sync_buffers(self.flat.bflat, self.pg)
             self._graph.replay()

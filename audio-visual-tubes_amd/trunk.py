@@ -478,7 +478,7 @@ class Trunk:
         return g, premasked
 
     def backward_stem(self, tape: Dict, g: torch.Tensor, store: Store):
-        """maxpool -> relu/bn1 -> stem wgrad (no input gradient is needed)."""
+        """maxpool -> relu/bn1 -> stem wgrad (and, when the tape asks for it, the input gradient)."""
         drive(self.backward_stem_iter(tape, g, store))
 
     def backward_stem_iter(self, tape: Dict, g: torch.Tensor, store: Store):
@@ -493,3 +493,8 @@ class Trunk:
              N, H1, W1, 64, stream_ptr())
         yield
         self._wgrad(tape["x"], g_c0, N, tape["H"], tape["W"], self.stem, store)
+        if tape.get("want_dx"):  # d(loss)/d(input), NCHW fp32 (a standalone trunk whose input requires grad)
+            gx = torch.empty(N, self.stem.cin, tape["H"], tape["W"], device=g_c0.device, dtype=torch.float32)
+            call("avt_conv_stem_dgrad", P(g_c0), P(store.param(self.stem.name)), P(gx), N, tape["H"], tape["W"],
+                 self.stem.cin, stream_ptr())
+            tape["dx"] = gx

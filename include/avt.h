@@ -144,6 +144,11 @@ size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K,
 int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
                      int S, int stride, int pad, void* workspace, size_t ws_bytes, void* stream);
 
+/* Input gradient of the 7x7 / stride 2 / pad 3 stem conv (base_models.py:135-138, the reference's autograd through
+ * conv1 / conv1_a when the trunk input requires grad): gx[N][Cin][H][W] fp32 (NCHW, the input's layout) =
+ * conv2d_input(gy[N,P,Q,64] bf16, w fp32 OHWI [64][7][7][Cin]); Cin <= 4; fp32 sums over (r, s, k) in a fixed order. */
+int avt_conv_stem_dgrad(const void* gy, const float* w, float* gx, int N, int H, int W, int Cin, void* stream);
+
 /* Conv3d, temporal stride 1: y[N,T',P,Q,K] = conv3d(x[N,T,H,W,Cp], wpack[K][(kt,r,s,c)]),
  * T' = T + 2*pad_t - KT + 1, spatial stride 1 or 2; Cp % 32 == 0; KT*R*S <= 27; bn_acc as conv2d_fwd */
 int avt_conv3d_fwd(const void* x, const void* wpack, void* y, double* bn_acc, int N, int T, int H, int W, int Cp,

@@ -34,9 +34,6 @@ int avt_set_halo(int on);
  * tile where it measured faster (C >= 512, or 256-row tiles fitting one wave of blocks); 0: the 4-wave
  * 128x128 tile for every W <= 19 shape; -1: back to the environment default — an A/B knob */
 int avt_set_halo8(int on);
-/* 1: the halo fwd/dgrad tiles run on v_mfma_f32_16x16x32_bf16 (2x2 per 32x32 block) instead of 32x32x16;
- * 0: 32x32x16; -1: the environment default (AVT_HALO_MF16) — an A/B knob (fp32 sums in another order) */
-int avt_set_halo_mf16(int on);
 /* weight-ring stages of the 8-wave 256x128 halo tile: 3 (default) or 4 (150 KB of LDS, still one block per
  * CU); -1: the environment default (AVT_HALO8_NST) — an A/B knob (bitwise the same results) */
 int avt_set_halo8_nst(int nst);
@@ -44,13 +41,6 @@ int avt_set_halo8_nst(int nst);
  * LDS reads per MFMA, one wave per SIMD); -1: the environment default (AVT_HALO8_FORM) — an A/B knob
  * (bitwise the same outputs; the BN statistics summed over another wave partition) */
 int avt_set_halo8_form(int form);
-/* the 8-wave halo tiles' SIMD-partner stagger: bit 0 = waves 4-7 run each tap step's last k-step of MFMAs
- * after the next barrier (bitwise the same results), bit 1 = waves 4-7 at s_setprio 1 in the main loop;
- * -1: the environment default (AVT_HALO_STAG, 0) — an A/B knob */
-int avt_set_halo_stagger(int mode);
-/* the same for the 8-wave TN wgrad blocks (the 256-wide layer4 tiles and the two-group 128 x 128 pairs);
- * -1: the environment default (AVT_WGRAD_STAG, 0) — an A/B knob */
-int avt_set_wgrad_stagger(int mode);
 /* 1 (default; env AVT_C64): 3x3 stride-1 fwd/dgrad with C = K = 64 (the layer-1 convs, image width <= 95)
  * run on the persistent kernel whose 64 x 576 weight operand stays resident in LDS (halo patch per
  * 256-pixel tile); 0: the tap-gather kernel (also off whenever avt_set_halo(0)) — an A/B knob */

@@ -245,6 +245,45 @@ def test_standalone_trunks_forward_backward():
         assert params["conv1_flow.weight"].grad is None and params["fc.weight"].grad is None
 
 
+def test_standalone_trunk_input_gradient():
+    """A trunk whose input requires grad (base_models.py:195-210 under the reference's autograd, which returns
+    d(loss)/dx through conv1 / conv1_a): x.grad of <map, R> vs the fp64 oracle trunk's, within 3x the deviation of
+    the oracle's own trunk in bf16 autocast; the parameter gradients are the same as without the input gradient."""
+    img, aud = _tiny()
+    model = _model()
+    for net, x, prefix, modal in ((model.imgnet, img, "imgnet.", "vision"), (model.audnet, aud, "audnet.", "audio")):
+        g = torch.Generator().manual_seed(4)
+        xd = x.to(DEV).requires_grad_(True)
+        out = net(xd)
+        R = torch.randn(out.shape, generator=g)
+        (out * R.to(DEV)).sum().backward()
+        gw = {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None}
+        for p_ in net.parameters():
+            p_.grad = None
+        out2 = net(x.to(DEV))
+        (out2 * R.to(DEV)).sum().backward()
+        for n, p_ in net.named_parameters():  # the input gradient changes nothing else
+            if p_.grad is not None:
+                assert torch.equal(p_.grad, gw[n]), n
+
+        def ref_dx(sd, xx, bf16):
+            xx = xx.clone().requires_grad_(True)
+            if bf16:
+                with torch.autocast("cpu", dtype=torch.bfloat16):
+                    y = orc.resnet18_forward(sd, prefix, xx, modal, training=True).float()
+            else:
+                y = orc.resnet18_forward(sd, prefix, xx, modal, training=True)
+            (y * R.to(y.dtype)).sum().backward()
+            return xx.grad
+
+        d64 = ref_dx(_sd64(), x.double(), False)
+        dbf = ref_dx(orc.make_state(0), x, True)
+        e, eb = rel_err(xd.grad, d64), rel_err(dbf, d64)
+        print(f"{modal}: dL/dx rel err {e:.3e} (bf16 reference {eb:.3e})")
+        assert xd.grad.shape == x.shape and xd.grad.dtype == torch.float32
+        assert e <= max(2e-2, 3 * eb), (modal, e, eb)
+
+
 # ------------------------------------------------------------------------------------------ step
 def test_lr_change_after_capture_reaches_replays():
     """Adam's hyper-parameters are read on the device by every replay (MultiStepLR)."""

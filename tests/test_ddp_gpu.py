@@ -138,7 +138,8 @@ def _seg_vs_eager(B=2, seed=0):
     m = _model(dev)
     step = HardWayTrainStep(m, lr=1e-6, weight_decay=1e-4)
     step.world, step.overlap = 2, True  # take the segmented-capture path (two streams); collectives are no-ops
-    step._allreduce_bucket = lambda tag, works: None
+    step._dp_boundary = lambda tags, pending: None  # no collectives (one process) and no Adam: gradients only
+    step._dp_finish = lambda pending: None
     img, aud = orc.make_image(B, 64).to(dev), orc.make_spectrogram(B, 65, 76).to(dev)
     for _ in range(2):
         step.step(img, aud)

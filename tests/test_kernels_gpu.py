@@ -114,16 +114,8 @@ def tiles(request):
     call("avt_set_small_tiles", 1)
 
 
-@pytest.fixture(params=[0, 1], ids=["mfma32", "mfma16"])
-def mf16(request):
-    """Run the halo fwd/dgrad tiles on 32x32x16 MFMAs, then on 16x16x32 ones (avt_set_halo_mf16)."""
-    call("avt_set_halo_mf16", request.param)
-    yield request.param
-    call("avt_set_halo_mf16", -1)
-
-
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_and_bn_partials(case, tiles, mf16):
+def test_conv_fwd_and_bn_partials(case, tiles):
     N, H, W, C, K, R, st, pad = case
     x = _rand_act(N, H, W, C, 1).relu()
     g = torch.Generator().manual_seed(2)
@@ -218,10 +210,9 @@ def test_halo_matches_gather(case):
     dy = _rand_act(N, H, W, K, 43).to(DEV)
     outs = []
     try:
-        for halo, halo8, m16 in ((0, 1, 0), (1, 0, 0), (1, 1, 0), (2, 1, 0), (1, 0, 1), (1, 1, 1), (2, 1, 1)):
+        for halo, halo8 in ((0, 1), (1, 0), (1, 1), (2, 1)):
             call("avt_set_halo", halo)
             call("avt_set_halo8", halo8)
-            call("avt_set_halo_mf16", m16)
             y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
             acc = fwd_acc(N * H * W, K)
             call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
@@ -232,7 +223,6 @@ def test_halo_matches_gather(case):
     finally:
         call("avt_set_halo", 1)
         call("avt_set_halo8", -1)
-        call("avt_set_halo_mf16", -1)
     (y0, dx0, a0) = outs[0]
     # 4-wave 128x128 and 8-wave 256x128 halo forms for W <= 19 (avt_set_halo8), the 8-wave forms for W <= 79
     for y1, dx1, a1 in outs[1:]:
@@ -385,7 +375,7 @@ def test_stem_fwd_wgrad(cin, cp, H, W, N):
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_dgrad(case, tiles, mf16):
+def test_conv_dgrad(case, tiles):
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     dy = _rand_act(N, Pq, Qq, K, 5)
@@ -918,7 +908,7 @@ def _bn_stats_rand(C, seed):
 
 @pytest.mark.parametrize("case", CONV_CASES)
 @pytest.mark.parametrize("mode", ["relu_fma", "mask_y", "two_bn"])
-def test_conv_dgrad_bn_epilogue(case, mode, mf16):
+def test_conv_dgrad_bn_epilogue(case, mode):
     """avt_conv2d_dgrad_bn: the store epilogue masks the dgrad result by the BN's ReLU (recomputed from
     (xc, scale, shift) or read from y) and accumulates that BN's backward reductions (and a second
     BN's) -- bitwise the masked plain-dgrad result, sums == fp64 sums of it; then
@@ -1024,61 +1014,6 @@ def test_strided_dgrad_skip00_then_downsample_epilogue(case):
     tol = 1e-5 * gm.abs().sum((0, 1, 2)).max().item() + 1e-6
     np.testing.assert_allclose(a[:, 0].numpy(), s1.numpy(), atol=tol)
     np.testing.assert_allclose(a[:, 1].numpy(), s2.numpy(), atol=tol * 4)
-
-
-@pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (5, 14, 14, 512, 512, 3, 1, 1),
-                                  (2, 33, 38, 128, 128, 3, 1, 1), (1, 28, 28, 128, 128, 3, 1, 1)])
-def test_halo_stagger_bitwise_equal(case, mf16):
-    """The 8-wave halo tiles' SIMD-partner stagger (avt_set_halo_stagger: waves 4-7 run each tap step's last
-    k-step after the next barrier, and/or at s_setprio 1) moves MFMAs in time, not in accumulation order:
-    outputs, dgrads (plain and with the BN epilogue's mask) and BN partial sums are bitwise equal."""
-    N, H, W, C, K, R, st, pad = case
-    x = _rand_act(N, H, W, C, 61).relu().to(DEV)
-    g = torch.Generator().manual_seed(62)
-    w = (torch.randn(K, R, R, C, generator=g) * 0.05).float().to(DEV)
-    wf, wt = pack(w, C, R * R * C)
-    dy = _rand_act(N, H, W, K, 63).to(DEV)
-    call("avt_set_halo8", 1)
-    outs = []
-    try:
-        for mode in (0, 1, 2, 3):
-            call("avt_set_halo_stagger", mode)
-            y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
-            acc = fwd_acc(N * H * W, K)
-            call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
-            dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
-            call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st, pad, S())
-            torch.cuda.synchronize()
-            outs.append((y.view(torch.int16).clone(), dx.view(torch.int16).clone(), acc_sums(acc, K, 3)))
-    finally:
-        call("avt_set_halo_stagger", -1)
-        call("avt_set_halo8", -1)
-    for o in outs[1:]:
-        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
-        assert torch.equal(o[2], outs[0][2])
-
-
-@pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (8, 14, 14, 256, 512, 3, 1, 1),
-                                  (2, 33, 38, 128, 128, 3, 1, 1), (4, 28, 28, 128, 128, 3, 1, 1)])
-def test_wgrad_stagger_bitwise_equal(case):
-    """The 8-wave TN wgrad blocks' stagger (avt_set_wgrad_stagger; the 256-wide layer4 tiles and the two-group
-    128 x 128 pairs) changes when MFMAs run, not the order they accumulate in: dw is bitwise equal, and the
-    deterministic slab reduce makes repeated runs bitwise equal too."""
-    N, H, W, C, K, R, st, pad = case
-    x = _rand_act(N, H, W, C, 71).relu().to(DEV)
-    dy = _rand_act(N, H, W, K, 72).to(DEV)
-    outs = []
-    try:
-        for mode in (0, 0, 1, 2, 3):
-            call("avt_set_wgrad_stagger", mode)
-            dw = torch.zeros(K, R, R, C, device=DEV)
-            wgrad(x, dy, dw, N, H, W, C, C, K, R, st, pad)
-            torch.cuda.synchronize()
-            outs.append(dw.clone())
-    finally:
-        call("avt_set_wgrad_stagger", -1)
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
 
 
 @pytest.mark.parametrize("case", [(32, 17, 19, 256, 256, 3, 1, 1), (32, 14, 14, 256, 256, 3, 1, 1),
@@ -1203,3 +1138,18 @@ def test_bn_finalize_rejects_bad_slot_header(header):
     torch.cuda.synchronize()
     assert torch.isnan(stats[2]).all() and torch.isnan(stats[3]).all()
     assert torch.isnan(dbeta).all() and torch.isnan(dgamma).all()
+
+
+@pytest.mark.parametrize("N,H,W,Cin", [(2, 20, 22, 3), (2, 21, 17, 1), (1, 224, 224, 3), (2, 9, 8, 3)])
+def test_stem_dgrad(N, H, W, Cin):
+    """avt_conv_stem_dgrad: the 7x7 / s2 / p3 stem conv's input gradient (base_models.py:135-138 under autograd) vs
+    torch's conv2d_input in fp64 on the same bf16 output gradient and fp32 weights."""
+    P_, Q_ = conv_out(H, 7, 2, 3), conv_out(W, 7, 2, 3)
+    gy = _rand_act(N, P_, Q_, 64, 91)
+    w = torch.randn(64, 7, 7, Cin, generator=torch.Generator().manual_seed(92)) * 0.05  # OHWI
+    gx = torch.empty(N, Cin, H, W, device=DEV)
+    call("avt_conv_stem_dgrad", P(D(gy)), P(D(w.contiguous())), P(gx), N, H, W, Cin, S())
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double().permute(0, 3, 1, 2), gy.double().permute(0, 3, 1, 2),
+                                     stride=2, padding=3)
+    assert rel_err(gx, ref) < 1e-5

@@ -48,7 +48,7 @@ typedef void (*Launcher)(const GemmNTParams&, const HaloArgs&, int, hipStream_t)
 
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF>
 void launch_v(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false, false, 0, PREF>), dim3(grid),
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false, PREF>), dim3(grid),
                      dim3(WM * WN * 64), 0, st, p, ha);
 }
 

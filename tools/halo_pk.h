@@ -105,7 +105,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     const int pr = q * RPI + lrow;
     const int pix = pbase + pr;
     const bool ok = pr < PR && pix >= 0 && pix < p.M;
-    const int lc = pchunk ^ halo_swz<false>(pr);
+    const int lc = pchunk ^ halo_swz(pr);
     return ok ? (unsigned)((pix * p.IC + cofs + lc * 8) * 2) : kOOB;  // 32-bit: activations stay below 2 GiB
   };
   // the patch pieces' lane terms (piece k, instruction a: patch row pr = q * 8 + lrow, q = (k AP + a) NW + wid):
@@ -117,13 +117,13 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     const int q = k * NW + wid;
     const int pr = q * RPI + lrow;
     prr[k] = pr;
-    pl[k] = (q < PINSTR && pr < PR) ? (pr * p.IC + (pchunk ^ halo_swz<false>(pr)) * 8) * 2 : -1;
+    pl[k] = (q < PINSTR && pr < PR) ? (pr * p.IC + (pchunk ^ halo_swz(pr)) * 8) * 2 : -1;
   }
   unsigned b_row[BR];  // weight DMA offset of this lane's row, without the tile's column base
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
     const int row = (wid * BR + i) * RPI + lrow;
-    const int lc = pchunk ^ halo_swz<false>(row);
+    const int lc = pchunk ^ halo_swz(row);
     b_row[i] = (unsigned)(((size_t)row * p.Kg + lc * 8) * 2);
   }
   const int frow = lane & (FR - 1), fhalf = lane / FR;
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int row = wn * (BN / WN) + j * FR + frow;
-      boffs[j][ks] = row * RB + (((2 * ks + fhalf) ^ halo_swz<false>(row)) << 4);
+      boffs[j][ks] = row * RB + (((2 * ks + fhalf) ^ halo_swz(row)) << 4);
     }
   // A row address of every (tap, row block) for the tile at m0 (conv_halo_kernel's arow; recomputed per item)
   unsigned arow[9][FM];
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const int y = oh + tdy(t), x = ow + tdx(t);
         const bool v = ok && y >= 0 && y < H && x >= 0 && x < W;
         const int pr = row + pre + tdy(t) * W + tdx(t);
-        arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((sfh ^ halo_swz<false>(pr)) << 4));
+        arow[t][i] = (unsigned)((v ? pr * RB : PRMAX * RB + (pr & 7) * RB) | ((sfh ^ halo_swz(pr)) << 4));
       }
     }
   };
