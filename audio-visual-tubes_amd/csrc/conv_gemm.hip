@@ -263,14 +263,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(GemmNTParams p) {
 // ------------------------------------------------------------------------------------------------
 // TN kernel (wgrad): DW[k_out][col] += sum_pix DY[pix][k_out] * X(pix, col)
 // ------------------------------------------------------------------------------------------------
-struct GemmTNParams {
-  const bf16_t* dy;  // [Kred][Mg]
-  const bf16_t* x;   // [N][H][W][Cp]
-  float* dw;         // [Mg][R*S*Creal] fp32 (atomic accumulate)
-  int Mg, Ng, Kred;  // Ng = padded patch width (multiple of BN)
-  int H, W, Cp, Creal, P, Q, R, S, stride, pad;
-  int kt_per_split;
-};
 
 template <int CVEC, int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(GemmTNParams p) {
@@ -479,9 +471,9 @@ static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epil
 static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
 static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
-static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel: -1 = env AVT_WGRAD_HALO (default 0:
-                                   // measured 230-320 TFLOP/s vs 450-820 for the tap-gather kernel, see
-                                   // conv_wgrad_halo.h)
+static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel (conv_wgrad_halo.h): 0 off, 1 nine taps per
+                                   // block, 2 one filter row per block, 3 (default) the one-row form for K = 64
+                                   // (layer 1: 480-550 -> 670-715 TFLOP/s), tap-gather elsewhere; -1 = env AVT_WGRAD_HALO
 static int num_cus() {
   static int n = 0;
   if (n == 0) {
@@ -1476,37 +1468,65 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
 }
 
 // ---- halo wgrad plan (conv_wgrad_halo.h) ----
+static int g_wgrad_halo_rw = -1;  // rows per wave of the K = 64 halo wgrad: 32 (default) or 64; -1: env AVT_WGRAD_HALO_RW
+static int wgrad_halo_rw() {
+  if (g_wgrad_halo_rw < 0) g_wgrad_halo_rw = getenv("AVT_WGRAD_HALO_RW") ? atoi(getenv("AVT_WGRAD_HALO_RW")) : 32;
+  return g_wgrad_halo_rw;
+}
+static int g_row3_min_kt = -1;  // ROW3 split floor (k-tiles per split); -1: env AVT_ROW3_MIN_KT
+static int row3_min_kt() {
+  if (g_row3_min_kt < 0) g_row3_min_kt = getenv("AVT_ROW3_MIN_KT") ? atoi(getenv("AVT_ROW3_MIN_KT")) : 8;
+  if (g_row3_min_kt < 1) g_row3_min_kt = 1;
+  return g_row3_min_kt;
+}
 static int wgrad_halo_enabled() {
   if (g_wgrad_halo < 0) {
     const char* e = getenv("AVT_WGRAD_HALO");
-    g_wgrad_halo = e ? atoi(e) : 0;
+    g_wgrad_halo = e ? atoi(e) : 3;
   }
   return g_wgrad_halo;
 }
 
 struct WgradHaloPlan {
   bool ok;
-  int WM;  // 2: BM 128 (4 waves), 1: BM 64 (2 waves); one wave per SIMD
+  bool row3; // one filter row (3 taps) per block: WM x 2 waves of 64 x 96, strip of PR - 2 PW patch rows
+  int WM;    // 2: BM 128 (4 waves), 1: BM 64 (2 waves)
+  int RW;    // output channels per wave: 64, or 32 (9-tap form, K = 64: 4 waves of 32 x 288, two per SIMD)
   WgradHaloArgs a;
   size_t slab_bytes;
-  int groups, per_group;  // reduce: split groups
+  int groups, per_group;  // reduce: split groups (pass 1), then one ordered pass over the group heads
 };
+
+static constexpr int kRow3PrMax = 40;  // strip rows staged by the ROW3 form
+// default form 3 takes ROW3 from this many output pixels up (B = 128: 401 k vision / 624 k audio); below
+// it the fixed cost of the split partials (slab + ordered reduce) loses to the tap-gather kernel (B = 32:
+// 100 k / 156 k pixels, -1.5 % per step in a same-box A/B)
+static constexpr long long kRow3MinPixels = 200000;
 
 static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad) {
   WgradHaloPlan pl{};
   pl.ok = false;
-  if (!wgrad_halo_enabled() || R != 3 || S != 3 || stride != 1 || pad != 1 || Cp != Creal || Cp % 64 != 0 ||
+  int mode = wgrad_halo_enabled();
+  if (mode == 3) mode = (K == 64 && (long long)N * H * W >= kRow3MinPixels) ? 2 : 0;
+  if (!mode || R != 3 || S != 3 || stride != 1 || pad != 1 || Cp != Creal || Cp % 64 != 0 ||
       K % 64 != 0 || conv_variant() != 1)
     return pl;
   WgradHaloArgs& a = pl.a;
   a.N = N; a.H = H; a.W = W; a.C = Cp; a.K = K;
+  pl.row3 = mode == 2;
   pl.WM = (K % 128 == 0) ? 2 : 1;
-  const int BM = pl.WM * 64;
-  const int PRMAX = pl.WM == 2 ? 160 : 72;
-  const int per_cu = pl.WM == 2 ? 1 : 2;  // resident blocks: one wave per SIMD (288 accumulator registers)
-  // cost of a k-tile: MFMA cycles of a block (4 SIMDs) vs its share of the ~29 B/clk L2->LDS fill
-  const double t_mfma = 2.0 * 32 * BM * 576 / (4 * 1024.0);
-  auto cost = [&](long long tiles, int pr) {
+  pl.RW = 64;
+  if (!pl.row3 && K == 64 && wgrad_halo_rw() == 32) {  // 4 waves of 32 x 288 (144 accumulator registers: two waves per SIMD)
+    pl.WM = 2;
+    pl.RW = 32;
+  }
+  const int BM = pl.WM * pl.RW;
+  const int ncols = pl.row3 ? 192 : 576;  // GEMM columns per block
+  const int PRMAX = pl.row3 ? kRow3PrMax : (pl.WM == 2 && pl.RW == 64) ? 160 : 72;
+  const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 : 2) : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
+  auto staged = [&](int pr, int pw) { return pl.row3 ? pr - 2 * pw : pr; };
+  const double t_mfma = 2.0 * 32 * BM * ncols / (4 * 1024.0);
+  auto cost = [&](long long tiles, int pr) {  // pr: staged patch rows
     const double fill = (32.0 * BM * 2 + pr * 128.0) / (29.0 / per_cu);
     return (double)tiles * (t_mfma > fill ? t_mfma : fill);
   };
@@ -1515,9 +1535,9 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   {
     const int span = (W >= 32 ? 2 : (31 + W - 1) / W + 1);
     const int pr = (span + 2) * (W + 2);
-    if (pr <= PRMAX) {
+    if (!pl.row3 && staged(pr, W + 2) <= PRMAX) {  // (ROW3: windows only -- fixed fragment rows)
       const long long tiles = (long long)(H * W + 31) / 32;
-      best = cost(tiles, pr);
+      best = cost(tiles, staged(pr, W + 2));
       a.raster = 1; a.R = 1; a.CW = 32; a.lcw = 5; a.wcols = 1; a.tiles_img = (int)tiles; a.PW = W + 2; a.PR = pr;
     }
   }
@@ -1525,9 +1545,9 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   for (auto& sh : shapes) {
     const int r = sh[0], cw = sh[1];
     const int pr = (r + 2) * (cw + 2);
-    if (pr > PRMAX) continue;
+    if (staged(pr, cw + 2) > PRMAX) continue;
     const int bands = (H + r - 1) / r, wcols = (W + cw - 1) / cw;
-    const double c = cost((long long)bands * wcols, pr);
+    const double c = cost((long long)bands * wcols, staged(pr, cw + 2));
     if (best < 0 || c < best * 0.999) {
       best = c;
       a.raster = 0; a.R = r; a.CW = cw; a.lcw = 31 - __builtin_clz(cw); a.wcols = wcols; a.tiles_img = bands * wcols;
@@ -1536,9 +1556,13 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   }
   if (best < 0) return pl;
   a.nkt = N * a.tiles_img;
-  const int per_split = (K / BM) * (Cp / 64);
+  const int per_split = (K / BM) * (Cp / 64) * (pl.row3 ? 3 : 1);
   const long long slots = (long long)num_cus() * per_cu;
   int splits = (int)(slots / per_split);
+  if (pl.row3) {  // at least row3_min_kt() k-tiles per split: the slab (splits x 147 KB at K 64) is the cost at small N
+    const int cap = a.nkt / row3_min_kt();
+    if (splits > cap) splits = cap;
+  }
   if (splits < 1) splits = 1;
   if (splits > a.nkt) splits = a.nkt;
   const int kps = (a.nkt + splits - 1) / splits;
@@ -1546,10 +1570,11 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   a.splits = (a.nkt + kps - 1) / kps;  // every split non-empty
   a.div_w = make_magic((unsigned)W);
   a.div_tiles = make_magic((unsigned)a.tiles_img);
+  a.div_wcols = make_magic((unsigned)a.wcols);
   a.dy_bytes = (unsigned)((size_t)N * H * W * K * 2);
   a.x_bytes = (unsigned)((size_t)N * H * W * Cp * 2);
   pl.slab_bytes = a.splits > 1 ? (size_t)a.splits * K * 9 * Cp * sizeof(float) : 0;
-  pl.per_group = 32;
+  pl.per_group = 16;
   pl.groups = (a.splits + pl.per_group - 1) / pl.per_group;
   pl.ok = true;
   return pl;
@@ -1562,21 +1587,32 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
   a.dy = dy;
   a.dw = dw;
   a.slab = slab;
-  const int BM = pl.WM * 64;
-  const int grid = (a.K / BM) * (a.C / 64) * a.splits;
-  if (pl.WM == 2)
+  const int BM = pl.WM * pl.RW;
+  const int grid = (a.K / BM) * (a.C / 64) * (pl.row3 ? 3 : 1) * a.splits;
+  if (pl.row3 && pl.WM == 2)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(256), 0, st, a);
+  else if (pl.row3)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(128), 0, st, a);
+  else if (pl.RW == 32)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 6, 72, 32>), dim3(grid), dim3(256), 0, st, a);
+  else if (pl.WM == 2)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 5, 160>), dim3(grid), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 6, 72>), dim3(grid), dim3(128), 0, st, a);
-  if (slab) {
+  if (slab) {  // ordered: groups of per_group splits, then the group heads
     const long long n = (long long)a.K * 9 * a.C;
-    dim3 rg((unsigned)((n / 4 + 255) / 256), (unsigned)pl.groups);
-    hipLaunchKernelGGL(wgrad_halo_reduce_kernel, rg, dim3(256), 0, st, slab, a.splits, pl.per_group, n, dw);
+    const unsigned gx = (unsigned)((n / 4 + 255) / 256);
+    if (pl.groups > 1)
+      hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx, (unsigned)pl.groups), dim3(256), 0, st, slab, a.splits, 1,
+                         pl.per_group, n, dw);
+    hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx, 1), dim3(256), 0, st, slab, pl.groups > 1 ? pl.groups : a.splits,
+                       pl.groups > 1 ? pl.per_group : 1, pl.groups > 1 ? pl.groups : a.splits, n, dw);
   }
 }
 
 extern "C" int avt_set_wgrad_halo(int on) {
-  avt::g_wgrad_halo = on ? 1 : 0;
+  AVT_REQUIRE(on >= 0 && on <= 3, "avt_set_wgrad_halo: %d (0 off, 1 nine taps, 2 one filter row per block, 3 = 2 for K 64)", on);
+  avt::g_wgrad_halo = on;
   return AVT_OK;
 }
 

@@ -1,4 +1,4 @@
-// The NT (fwd / dgrad) conv kernels' parameter block, shared by conv_gemm.hip and the standalone kernel
+// The conv kernels' parameter blocks (NT fwd / dgrad, TN wgrad), shared by conv_gemm.hip and the standalone kernel
 // benches under tools/ (included inside namespace avt).
 #pragma once
 
@@ -44,3 +44,13 @@ struct GemmNTParams {
 __device__ __forceinline__ int swz64(int row, int chunk) {  // byte offset in a [rows][32 bf16] tile
   return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
 }
+
+// wgrad ("TN"): dw[Mg][R*S*Creal] += sum over the Kred output pixels of dy[pix][Mg] * x[gathered pixel][(r,s,c)]
+struct GemmTNParams {
+  const bf16_t* dy;  // [Kred][Mg]
+  const bf16_t* x;   // [N][H][W][Cp]
+  float* dw;         // [Mg][R*S*Creal] fp32 (atomic accumulate)
+  int Mg, Ng, Kred;  // Ng = padded patch width (multiple of BN)
+  int H, W, Cp, Creal, P, Q, R, S, stride, pad;
+  int kt_per_split;
+};

@@ -20,14 +20,20 @@
 // k-tiles; partials go to an fp32 slab (plain stores) reduced by wgrad_halo_reduce_kernel, or fp32
 // atomics without a workspace.
 //
-// STATUS: correct (tests/test_kernels_gpu.py runs every 3x3/s1 wgrad case through it) but SLOWER
-// than the tap-gather kernel (230-320 vs 450-820 TFLOP/s at the trunk shapes), so it is off by
-// default (avt_set_wgrad_halo / AVT_WGRAD_HALO=1).  Why: a wave tile of 64 x 288 needs 288 fp32
-// accumulator registers; with 256 AGPRs the compiler shuffles accumulators through v_accvgpr moves
-// (~16 per MFMA in the k loop, SQ_INSTS_VALU/SQ_INSTS_MFMA = 33).  The 32 x 288 tile (144
-// registers, 2 waves/SIMD) has no spill but reads each B fragment in 4 waves (1.1 KB of LDS per
-// MFMA: LDS-bound).  The 9-tap N dimension does not split into a <= 256-register wave tile with
-// fragment reuse on both operands; a 32-channel-chunk / 3-tap-per-wave layout is the next try.
+// Forms.  Nine taps per block (avt_set_wgrad_halo(1)): each wave RW output channels x 9 of the 18
+// 32-column subtiles.  Slower than the tap-gather kernel (230-320 vs 450-820 TFLOP/s at the trunk shapes):
+// a wave tile of 64 x 288 needs 288 accumulator registers (the compiler shuffles them through
+// v_accvgpr moves, SQ_INSTS_VALU/SQ_INSTS_MFMA = 33), and the 32 x 288 tile reads each B fragment in 4
+// waves (1.1 KB of LDS per MFMA).  One filter row per block (ROW3; avt_set_wgrad_halo(2), and the
+// default for K = 64, the layer-1 convs): a block owns 64 output channels x the 3 taps of filter row fr x
+// 64 channels, stages the DY tile and only the patch rows row fr reads (R x (CW + 2) rows), and each of
+// its 2 waves holds 64 x 96 (3 taps x one 32-channel half; 96 accumulator registers, two waves per SIMD,
+// 2 A + 3 B fragment reads per 6 MFMAs).  What made it fast is the address arithmetic, not the tile:
+// windows only, so every fragment row is fixed per lane; DMA offsets = per-tile scalar base + fixed
+// per-lane offset; the k loop unrolled by the ring depth so every LDS address is a per-lane register +
+// immediate (VALU per k-tile ~110 -> ~45: layer-1 356 -> 493 (vision) and 411 -> 610 (audio) TFLOP/s
+// including the slab reduce; the kernel alone 671 / 715 TFLOP/s against 486 / 523 for the tap-gather
+// kernel on the same box).
 #pragma once
 
 struct WgradHaloArgs {
@@ -43,14 +49,20 @@ struct WgradHaloArgs {
   int tiles_img;     // k-tiles per image
   int PW, PR;        // patch row width / patch rows (pixels)
   int nkt, kt_per_split, splits;
-  MagicDiv div_w, div_tiles;
+  MagicDiv div_w, div_tiles, div_wcols;
 };
 
-// WM x 2 waves, one per SIMD (2 x 9 accumulator tiles = 288 registers per lane): BM = 64 WM
-template <int WM, int NST, int PRMAX>
-__global__ __launch_bounds__(WM * 2 * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// WM x 2 waves.  ROW3 = false: each wave RW output channels x 9 of the 18 column subtiles: RW = 64 (2 x 9
+// accumulator tiles = 288 registers per lane, one wave per SIMD) or 32 (9 tiles, 144 registers: two waves per
+// SIMD -- two blocks per CU).  ROW3 = true (RW = 64): the block owns one filter row fr (3 taps) and stages only
+// the patch rows that row reads (the "strip": PR - 2 PW rows); each wave 64 output channels x 3 taps x one
+// 32-channel half = 6 accumulator tiles, 2 A + 3 B fragment reads per 6 MFMAs.  BM = RW * WM
+template <int WM, int NST, int PRMAX, int RW = 64, bool ROW3 = false>
+__global__ __launch_bounds__(WM * 2 * 64) __attribute__((amdgpu_waves_per_eu(RW == 64 && !ROW3 ? 1 : 2, RW == 64 && !ROW3 ? 1 : 2)))
 void conv_wgrad_halo_kernel(WgradHaloArgs a) {
-  constexpr int NW = WM * 2, BM = WM * 64;
+  static_assert(!ROW3 || RW == 64, "ROW3 form: 64 rows per wave");
+  constexpr int NW = WM * 2, BM = WM * RW, TR = RW / 32;
+  constexpr int NS = ROW3 ? 3 : 9;                 // column subtiles per wave
   constexpr int AROWB = BM * 2;                    // bytes per DY row (pixel)
   constexpr int A_RPI = 1024 / AROWB;              // DY rows per 1 KiB DMA instruction
   constexpr int A_BYTES = 32 * AROWB;
@@ -67,10 +79,14 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid % WM, hn = wid / WM;  // 64-row slice of BM, half of the 18 column subtiles
-  const int ct_count = a.C / 64, per_split = (a.K / BM) * ct_count;
+  const int wm = wid % WM, hn = wid / WM;  // RW-row slice of BM, half of the 18 column subtiles
+  constexpr int NFR = ROW3 ? 3 : 1;  // filter rows split over blocks
+  const int ct_count = a.C / 64, per_split = (a.K / BM) * ct_count * NFR;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = lin / per_split, rest = lin - split * per_split;
+  const int split = lin / per_split;
+  int rest = lin - split * per_split;
+  const int fr = ROW3 ? rest % 3 : 0;
+  rest /= NFR;
   const int mt = rest / ct_count, ct = rest - mt * ct_count;
   const int m0 = mt * BM, c0 = ct * 64;
   const int kt_begin = split * a.kt_per_split;
@@ -78,6 +94,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   if (kt_begin >= kt_end) return;  // never with a slab: the plan leaves no empty split
   const int nk = kt_end - kt_begin;
   const int H = a.H, W = a.W, HW = H * W;
+  const int PRS = ROW3 ? a.PR - 2 * a.PW : a.PR;  // patch rows staged (ROW3: logical rows fr*PW .. +PRS)
 
   const __amdgpu_buffer_rsrc_t rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, (int)a.dy_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, (int)a.x_bytes, 0x00020000);
@@ -100,7 +117,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   for (int i = 0; i < PIW; ++i) {
     const int q = i * NW + wid;
     const int pr = q * 8 + lane / 8;
-    p_in[i] = q < PINSTR && pr < a.PR;
+    p_in[i] = q < PINSTR && pr < PRS;
     const int py = pr / a.PW;
     p_dy[i] = py;
     p_dx[i] = pr - py * a.PW;
@@ -116,14 +133,14 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
     const unsigned n = magic_div((unsigned)kt, a.div_tiles);
     const int ti = kt - (int)n * a.tiles_img;
     t.n = (int)n;
-    if (a.raster) {
+    if (!ROW3 && a.raster) {
       t.p0 = ti * 32;
       t.y0 = (int)magic_div((unsigned)t.p0, a.div_w);
       t.x0 = 0;
       t.yo = t.y0 - 1;
       t.xo = -1;
     } else {
-      const int band = ti / a.wcols;
+      const int band = (int)magic_div((unsigned)ti, a.div_wcols);
       t.p0 = 0;
       t.y0 = band * a.R;
       t.x0 = (ti - band * a.wcols) * a.CW;
@@ -133,16 +150,42 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
     return t;
   };
 
+  // ROW3 (windows only): a DMA lane's source offset is a per-tile scalar base plus a fixed per-lane offset
+  unsigned a_lo[AI];
+  int p_lo[PIW];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) a_lo[i] = (unsigned)((a_ky[i] * W + a_kx[i]) * a.K * 2) + a_colB[i];
+#pragma unroll
+  for (int i = 0; i < PIW; ++i) p_lo[i] = (p_dy[i] * W + p_dx[i]) * a.C * 2 + (int)p_colB[i];
+
   auto issue = [&](int kt, int stage) {
     char* As = smem + stage * STAGE;
     char* Ps = As + A_BYTES;
     const bool live = kt < kt_end;
     const Tile t = tile_of(live ? kt : kt_begin);
+    if constexpr (ROW3) {
+      const unsigned abase = (unsigned)(((t.n * H + t.y0) * W + t.x0) * a.K * 2);
+      const int py0 = t.yo + fr, hy = H - t.y0, wx = W - t.x0;
+      const int pbase = ((t.n * H + py0) * W + t.xo) * a.C * 2;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const bool ok = live && a_ky[i] < hy && a_kx[i] < wx;
+        buf_lds16(rs_dy, As + (wid * AI + i) * 1024, ok ? abase + a_lo[i] : kOOB);
+      }
+#pragma unroll
+      for (int i = 0; i < PIW; ++i) {
+        const int q = i * NW + wid;
+        const bool pok = live && p_in[i] && (unsigned)(py0 + p_dy[i]) < (unsigned)H &&
+                         (unsigned)(t.xo + p_dx[i]) < (unsigned)W;
+        buf_lds16(rs_x, q < PINSTR ? Ps + q * 1024 : junk, pok ? (unsigned)(pbase + p_lo[i]) : kOOB);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       int y, x;
       bool ok;
-      if (a.raster) {
+      if (!ROW3 && a.raster) {
         const int p = t.p0 + a_row[i];
         y = (int)magic_div((unsigned)p, a.div_w);
         x = p - y * W;
@@ -158,18 +201,18 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 #pragma unroll
     for (int i = 0; i < PIW; ++i) {
       const int q = i * NW + wid;
-      const int py = t.yo + p_dy[i], px = t.xo + p_dx[i];
+      const int py = t.yo + fr + p_dy[i], px = t.xo + p_dx[i];
       const bool pok = live && p_in[i] && (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W;
       buf_lds16(rs_x, q < PINSTR ? Ps + q * 1024 : junk,
                 pok ? (unsigned)(((t.n * H + py) * W + px) * a.C * 2) + p_colB[i] : kOOB);
     }
   };
 
-  f32x16 acc[2][9];
+  f32x16 acc[TR][NS];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TR; ++i)
 #pragma unroll
-    for (int s = 0; s < 9; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][s][v] = 0.f;
 
@@ -183,54 +226,72 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) issue(kt_begin + s, s);
 
-  for (int k = 0; k < nk; ++k) {
+  // patch row (tap centre) of a fragment pixel k = 16 ks + tr_row + 4 rr (j = 2 ks + rr); the window
+  // form's rows are the same for every k-tile (ROW3 plans only windows: computed once)
+  auto pixel_rows = [&](int kt, int* pb) {
+    const Tile t = tile_of(kt);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kk = 16 * (j >> 1) + tr_row + 4 * (j & 1);
+      int y, x;
+      if (!ROW3 && a.raster) {
+        const int p = min(t.p0 + kk, HW - 1);  // pixels past the image: any in-patch row (DY is 0)
+        y = (int)magic_div((unsigned)p, a.div_w);
+        x = p - y * W;
+      } else {
+        y = t.y0 + (kk >> a.lcw);
+        x = t.x0 + (kk & (a.CW - 1));
+      }
+      pb[j] = (y - t.yo) * a.PW + (x - t.xo);
+    }
+  };
+  int pb[4];
+  if (ROW3) pixel_rows(kt_begin, pb);
+
+  // one k-tile: rs = the stage it reads, is = the stage the DMA issued here fills
+  auto step = [&](int k, int rs, int is) {
     wait_vmcnt<(NST - 2) * LPT>();
     ring_barrier();
-    const char* As = smem + (k % NST) * STAGE;
+    const char* As = smem + rs * STAGE;
     const char* Ps = As + A_BYTES;
-    // patch row (tap centre) of this lane's 4 fragment pixels: k = 16 ks + tr_row + 4 rr
-    int pb[4];
-    {
-      const Tile t = tile_of(kt_begin + k);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int kk = 16 * (j >> 1) + tr_row + 4 * (j & 1);
-        int y, x;
-        if (a.raster) {
-          const int p = min(t.p0 + kk, HW - 1);  // pixels past the image: any in-patch row (DY is 0)
-          y = (int)magic_div((unsigned)p, a.div_w);
-          x = p - y * W;
-        } else {
-          y = t.y0 + (kk >> a.lcw);
-          x = t.x0 + (kk & (a.CW - 1));
-        }
-        pb[j] = (y - t.yo) * a.PW + (x - t.xo);
-      }
-    }
-    bf16x8 af[2][2];
+    if (!ROW3) pixel_rows(kt_begin + k, pb);
+    bf16x8 af[2][TR];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = wm * 64 + i * 32 + tr_col;
+      for (int i = 0; i < TR; ++i) {
+        const int c = wm * RW + i * 32 + tr_col;
         const char* a0 = As + (ks * 16 + tr_row) * AROWB + ((c >> 3) ^ a_sw) * 16 + (c & 7) * 2;
         s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
         s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * AROWB));
         short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[ks][i] = __builtin_bit_cast(bf16x8, tmp);
       }
-    issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);  // the stage read at step k-1: all waves passed
+    issue(kt_begin + k + NST - 1, is);  // the stage read at step k-1: all waves passed
     // all 9 B fragments of a k-step are read before its 18 MFMAs, and the next k-step's reads are
     // issued while those run (two fragment buffers): one wave per SIMD has no other wave to hide
     // the LDS latency behind
-    bf16x8 bfr[2][9];
+    bf16x8 bfr[2][NS];
+    // subtile s -> tap and channel half; row displacement from the logical patch row of the tap centre
+    // (ROW3: the staged strip starts at logical row fr*PW, so a tap of row fr sits PW rows up)
+    auto sub = [&](int s, int& tap, int& hh, int& disp) {
+      if (ROW3) {
+        tap = fr * 3 + s;
+        hh = hn;
+        disp = -a.PW + (s - 1);
+      } else {
+        const int cs = hn * 9 + s;  // column subtile: tap cs/2, channel half cs%2
+        tap = cs >> 1;
+        hh = cs & 1;
+        const int dyt = tap / 3 - 1, dxt = tap - (tap / 3) * 3 - 1;
+        disp = dyt * a.PW + dxt;
+      }
+    };
     auto load_b = [&](int ks, int buf) {
 #pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        const int cs = hn * 9 + s;  // column subtile: tap cs/2, channel half cs%2
-        const int tap = cs >> 1, hh = cs & 1;
-        const int dyt = tap / 3 - 1, dxt = tap - (tap / 3) * 3 - 1;
-        const int disp = dyt * a.PW + dxt;
+      for (int s = 0; s < NS; ++s) {
+        int tap, hh, disp;
+        sub(s, tap, hh, disp);
         const int rlo = pb[2 * ks] + disp, rhi = pb[2 * ks + 1] + disp;
         const int c = hh * 32 + tr_col;
         const char* b0 = Ps + rlo * 128 + (((c >> 3) ^ tn_swz<128>(rlo)) << 4) + (c & 7) * 2;
@@ -247,12 +308,22 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
       if (ks == 0) load_b(1, 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int s = 0; s < 9; ++s) {
-        acc[0][s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][0], bfr[ks][s], acc[0][s], 0, 0, 0);
-        acc[1][s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][1], bfr[ks][s], acc[1][s], 0, 0, 0);
-      }
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < TR; ++i)
+          acc[i][s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks][i], bfr[ks][s], acc[i][s], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  if constexpr (ROW3) {
+    // stages as compile-time constants: every LDS address is a fixed per-lane offset + immediate
+    for (int k0 = 0; k0 < nk; k0 += NST) {
+#pragma unroll
+      for (int u = 0; u < NST; ++u)
+        if (k0 + u < nk) step(k0 + u, u, (u + NST - 1) % NST);
+    }
+  } else {
+    for (int k = 0; k < nk; ++k) step(k, k % NST, (k + NST - 1) % NST);
   }
   wait_vmcnt<0>();
 
@@ -261,15 +332,22 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   float* dst = a.slab ? a.slab + (size_t)split * a.K * ldw : a.dw;
   const int frow = lane & 31, fhalf = lane >> 5;
 #pragma unroll
-  for (int s = 0; s < 9; ++s) {
-    const int cs = hn * 9 + s;
-    const int tap = cs >> 1, hh = cs & 1;
+  for (int s = 0; s < NS; ++s) {
+    int tap, hh;
+    if (ROW3) {
+      tap = fr * 3 + s;
+      hh = hn;
+    } else {
+      const int cs = hn * 9 + s;
+      tap = cs >> 1;
+      hh = cs & 1;
+    }
     const int col = tap * a.C + c0 + hh * 32 + frow;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TR; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int row = m0 + wm * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
+        const int row = m0 + wm * RW + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf;
         if (a.slab)
           dst[(size_t)row * ldw + col] = acc[i][s][v];
         else
@@ -278,20 +356,29 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   }
 }
 
-// dw[i] += sum_{s in this block's split group} slab[s][i]; blockIdx.y = split group (fp32 atomics
-// across groups, a plain add for a single group): deep split counts stay parallel
-__global__ __launch_bounds__(256) void wgrad_halo_reduce_kernel(const float* __restrict__ slab, int splits, int per_group,
-                                                                long long n, float* __restrict__ dw) {
+// Ordered two-pass reduction of the split partials (deterministic): entry e (e < count) is
+// slab[e * step * n ...].  blockIdx.y = group of per_group consecutive entries, summed in order; with
+// several groups each group's sum overwrites its first entry (pass 1), with one group it is added to dw
+// (pass 2 runs over the group heads: step = per_group of pass 1)
+__global__ __launch_bounds__(256) void wgrad_halo_reduce_kernel(float* __restrict__ slab, int count, int step,
+                                                                int per_group, long long n, float* __restrict__ dw) {
   const long long i = (blockIdx.x * 256LL + threadIdx.x) * 4;
   if (i >= n) return;
-  const int s0 = blockIdx.y * per_group, s1 = min(splits, s0 + per_group);
+  const int s0 = blockIdx.y * per_group, s1 = min(count, s0 + per_group);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int s = s0; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(slab + (size_t)s * n + i);
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {  // four loads in flight, added in entry order
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(slab + (size_t)(s + u) * step * n + i);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u];
+  }
+  for (; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(slab + (size_t)s * step * n + i);
   if (gridDim.y == 1) {
     f32x4 d = *reinterpret_cast<const f32x4*>(dw + i);
     *reinterpret_cast<f32x4*>(dw + i) = d + acc;
   } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) atomicAdd(dw + i + e, acc[e]);
+    *reinterpret_cast<f32x4*>(slab + (size_t)s0 * step * n + i) = acc;
   }
 }

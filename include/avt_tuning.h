@@ -66,7 +66,9 @@ int avt_set_wgrad_policy(int target_blocks, int min_ktiles);
 int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 /* 1 (default): layer4 wgrads (K_out 512) use 8-wave 256-wide tiles; 0: 4-wave tiles of at most 128 — A/B knob */
 int avt_set_wgrad_tiles(int big);
-/* 3x3/s1 wgrads on the halo-reuse kernel (1; env AVT_WGRAD_HALO) or the tap-gather one (0, default) */
+/* 3x3/s1 wgrads on the halo-reuse kernel -- 1: all 9 taps per block, 2: one filter row (3 taps) per
+ * block, 3 (default): form 2 for the K = 64 (layer-1) convs and the tap-gather kernel elsewhere -- or all
+ * on the tap-gather one (0); env AVT_WGRAD_HALO.  Returns AVT_EINVAL outside 0..3 */
 int avt_set_wgrad_halo(int on);
 /* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
  * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */

@@ -448,33 +448,41 @@ def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
 
 
 @pytest.mark.parametrize("nst", [(4, 3), (8, 5), (6, 4)], ids=["ring4", "ring8", "ring6"])
-@pytest.mark.parametrize("big", [1, 0, "halo"])
+@pytest.mark.parametrize("big", [1, 0, "halo", "halo3"])
 @pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_wgrad(case, slab, big, nst):
     """big: the 256-wide tap-gather tiles (1), 128-wide only (0), or the halo-reuse kernel for the
-    3x3/s1 cases ("halo", off by default; conv_wgrad_halo.h).  nst: ring depth of the 4-wave / 8-wave
-    tap-gather tiles (avt_set_wgrad_nst; the deep rings change the split plan too)."""
-    if big == "halo" and nst != (4, 3):
+    3x3/s1 cases, nine taps ("halo") or one filter row ("halo3") per block (off by default;
+    conv_wgrad_halo.h).  nst: ring depth of the 4-wave / 8-wave tap-gather tiles (avt_set_wgrad_nst;
+    the deep rings change the split plan too).  With the slab every form is run twice: bitwise equal."""
+    if str(big).startswith("halo") and nst != (4, 3):
         pytest.skip("ring depth does not apply to the halo wgrad")
+    hv = {"halo": 1, "halo3": 2}.get(big, 0)
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
     dy = _rand_act(N, Pq, Qq, K, 9)
     dw = torch.full((K, R, R, C), 0.25, device=DEV)  # accumulates into an existing gradient
+    dw2 = dw.clone()
     try:
-        call("avt_set_wgrad_tiles", 1 if big == "halo" else big)
-        call("avt_set_wgrad_halo", int(big == "halo"))
+        call("avt_set_wgrad_tiles", 1 if hv else big)
+        call("avt_set_wgrad_halo", hv)
         call("avt_set_wgrad_nst", *nst)
-        wgrad(x.to(DEV), dy.to(DEV), dw, N, H, W, C, C, K, R, st, pad, slab)
+        xd, dyd = x.to(DEV), dy.to(DEV)
+        wgrad(xd, dyd, dw, N, H, W, C, C, K, R, st, pad, slab)
+        if slab:
+            wgrad(xd, dyd, dw2, N, H, W, C, C, K, R, st, pad, slab)
     finally:
         call("avt_set_wgrad_tiles", 1)
-        call("avt_set_wgrad_halo", 0)
+        call("avt_set_wgrad_halo", 3)
         call("avt_set_wgrad_nst", 4, 3)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)
     torch.cuda.synchronize()
     assert rel_err(dw.permute(0, 3, 1, 2) - 0.25, ref) < 2e-4
+    if slab:
+        assert torch.equal(dw, dw2)
 
 
 def test_wgrad_large_splitk():

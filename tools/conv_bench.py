@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--nt64", default="", help="comma list of avt_set_nt64_config values to sweep")
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
-    ap.add_argument("--wgrad-halo", default="0", help="comma list of avt_set_wgrad_halo values to sweep")
+    ap.add_argument("--wgrad-halo", default="3", help="comma list of avt_set_wgrad_halo values to sweep")
     ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
     ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
@@ -208,7 +208,7 @@ def main():
                     call("avt_set_wgrad_nst", 4, 3)
                 call("avt_set_wgrad_policy", 0, 4)
                 call("avt_set_wgrad_tiles", 1)
-                call("avt_set_wgrad_halo", 0)
+                call("avt_set_wgrad_halo", 3)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")
