@@ -1479,6 +1479,11 @@ static int row3_min_kt() {
   if (g_row3_min_kt < 1) g_row3_min_kt = 1;
   return g_row3_min_kt;
 }
+static int g_row3_kg = -1;  // ROW3 k groups per block (1 or 2); -1: env AVT_ROW3_KG
+static int row3_kg() {
+  if (g_row3_kg < 0) g_row3_kg = getenv("AVT_ROW3_KG") ? atoi(getenv("AVT_ROW3_KG")) : 2;
+  return (g_row3_kg == 2 || g_row3_kg == 4) ? g_row3_kg : 1;
+}
 static int wgrad_halo_enabled() {
   if (g_wgrad_halo < 0) {
     const char* e = getenv("AVT_WGRAD_HALO");
@@ -1490,6 +1495,7 @@ static int wgrad_halo_enabled() {
 struct WgradHaloPlan {
   bool ok;
   bool row3; // one filter row (3 taps) per block: WM x 2 waves of 64 x 96, strip of PR - 2 PW patch rows
+  int kg;    // ROW3, WM 1: k groups per block (KG 2-wave groups on interleaved k-tiles, one partial per block)
   int WM;    // 2: BM 128 (4 waves), 1: BM 64 (2 waves)
   int RW;    // output channels per wave: 64, or 32 (9-tap form, K = 64: 4 waves of 32 x 288, two per SIMD)
   WgradHaloArgs a;
@@ -1514,6 +1520,7 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   WgradHaloArgs& a = pl.a;
   a.N = N; a.H = H; a.W = W; a.C = Cp; a.K = K;
   pl.row3 = mode == 2;
+  pl.kg = 1;
   pl.WM = (K % 128 == 0) ? 2 : 1;
   pl.RW = 64;
   if (!pl.row3 && K == 64 && wgrad_halo_rw() == 32) {  // 4 waves of 32 x 288 (144 accumulator registers: two waves per SIMD)
@@ -1523,7 +1530,9 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   const int BM = pl.WM * pl.RW;
   const int ncols = pl.row3 ? 192 : 576;  // GEMM columns per block
   const int PRMAX = pl.row3 ? kRow3PrMax : (pl.WM == 2 && pl.RW == 64) ? 160 : 72;
-  const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 : 2) : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
+  if (pl.row3 && getenv("AVT_ROW3_WM") && atoi(getenv("AVT_ROW3_WM")) == 1) pl.WM = 1;  // A/B: 64-row blocks at K >= 128
+  if (pl.row3 && pl.WM == 1) pl.kg = row3_kg();
+  const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 / pl.kg : 2) : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
   auto staged = [&](int pr, int pw) { return pl.row3 ? pr - 2 * pw : pr; };
   const double t_mfma = 2.0 * 32 * BM * ncols / (4 * 1024.0);
   auto cost = [&](long long tiles, int pr) {  // pr: staged patch rows
@@ -1591,6 +1600,10 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
   const int grid = (a.K / BM) * (a.C / 64) * (pl.row3 ? 3 : 1) * a.splits;
   if (pl.row3 && pl.WM == 2)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(256), 0, st, a);
+  else if (pl.row3 && pl.kg == 4)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 4>), dim3(grid), dim3(512), 0, st, a);
+  else if (pl.row3 && pl.kg == 2)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 2>), dim3(grid), dim3(256), 0, st, a);
   else if (pl.row3)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(128), 0, st, a);
   else if (pl.RW == 32)
@@ -1601,13 +1614,22 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 6, 72>), dim3(grid), dim3(128), 0, st, a);
   if (slab) {  // ordered: groups of per_group splits, then the group heads
     const long long n = (long long)a.K * 9 * a.C;
-    const unsigned gx = (unsigned)((n / 4 + 255) / 256);
+    const unsigned gx = (unsigned)((n / 4 + 255) / 256), gx64 = (unsigned)((n / 4 + 63) / 64);
     if (pl.groups > 1)
       hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx, (unsigned)pl.groups), dim3(256), 0, st, slab, a.splits, 1,
                          pl.per_group, n, dw);
-    hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx, 1), dim3(256), 0, st, slab, pl.groups > 1 ? pl.groups : a.splits,
+    // the final pass is latency-bound (one thread per 4 outputs, a serial chain of entries): 64-thread blocks
+    hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx64, 1), dim3(64), 0, st, slab, pl.groups > 1 ? pl.groups : a.splits,
                        pl.groups > 1 ? pl.per_group : 1, pl.groups > 1 ? pl.groups : a.splits, n, dw);
   }
+}
+
+extern "C" int avt_set_wgrad_row3(int kg, int min_kt) {
+  AVT_REQUIRE(kg == -1 || kg == 1 || kg == 2 || kg == 4, "avt_set_wgrad_row3: kg=%d (1, 2 or 4)", kg);
+  AVT_REQUIRE(min_kt == -1 || min_kt >= 1, "avt_set_wgrad_row3: min_kt=%d", min_kt);
+  if (kg > 0) g_row3_kg = kg;
+  if (min_kt > 0) g_row3_min_kt = min_kt;
+  return AVT_OK;
 }
 
 extern "C" int avt_set_wgrad_halo(int on) {

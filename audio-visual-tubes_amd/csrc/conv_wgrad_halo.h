@@ -57,10 +57,11 @@ struct WgradHaloArgs {
 // SIMD -- two blocks per CU).  ROW3 = true (RW = 64): the block owns one filter row fr (3 taps) and stages only
 // the patch rows that row reads (the "strip": PR - 2 PW rows); each wave 64 output channels x 3 taps x one
 // 32-channel half = 6 accumulator tiles, 2 A + 3 B fragment reads per 6 MFMAs.  BM = RW * WM
-template <int WM, int NST, int PRMAX, int RW = 64, bool ROW3 = false>
-__global__ __launch_bounds__(WM * 2 * 64) __attribute__((amdgpu_waves_per_eu(RW == 64 && !ROW3 ? 1 : 2, RW == 64 && !ROW3 ? 1 : 2)))
+template <int WM, int NST, int PRMAX, int RW = 64, bool ROW3 = false, int KG = 1>
+__global__ __launch_bounds__(WM * 2 * KG * 64) __attribute__((amdgpu_waves_per_eu(RW == 64 && !ROW3 ? 1 : 2, RW == 64 && !ROW3 ? 1 : 2)))
 void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   static_assert(!ROW3 || RW == 64, "ROW3 form: 64 rows per wave");
+  static_assert(KG == 1 || ROW3, "k groups: ROW3 form only");
   constexpr int NW = WM * 2, BM = WM * RW, TR = RW / 32;
   constexpr int NS = ROW3 ? 3 : 9;                 // column subtiles per wave
   constexpr int AROWB = BM * 2;                    // bytes per DY row (pixel)
@@ -74,11 +75,15 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   constexpr int STAGE = A_BYTES + P_BYTES;
   constexpr int LPT = AI + PIW;
   static_assert(PRMAX % 8 == 0, "PRMAX");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE + 1024];
-  char* junk = smem + NST * STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[KG * NST * STAGE + 1024];
+  char* junk = smem + KG * NST * STAGE;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // KG k groups of NW waves: group kg takes the block's k-tiles kg, kg + KG, ... on its own ring; the
+  // groups' partial tiles are summed in LDS (fixed order) before the one store per block
+  const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = wall / NW, wid = wall - kg * NW;
+  char* ring = smem + kg * NST * STAGE;
   const int wm = wid % WM, hn = wid / WM;  // RW-row slice of BM, half of the 18 column subtiles
   constexpr int NFR = ROW3 ? 3 : 1;  // filter rows split over blocks
   const int ct_count = a.C / 64, per_split = (a.K / BM) * ct_count * NFR;
@@ -159,7 +164,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   for (int i = 0; i < PIW; ++i) p_lo[i] = (p_dy[i] * W + p_dx[i]) * a.C * 2 + (int)p_colB[i];
 
   auto issue = [&](int kt, int stage) {
-    char* As = smem + stage * STAGE;
+    char* As = ring + stage * STAGE;
     char* Ps = As + A_BYTES;
     const bool live = kt < kt_end;
     const Tile t = tile_of(live ? kt : kt_begin);
@@ -224,7 +229,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s) issue(kt_begin + s, s);
+  for (int s = 0; s < NST - 1; ++s) issue(kt_begin + s * KG + kg, s);
 
   // patch row (tap centre) of a fragment pixel k = 16 ks + tr_row + 4 rr (j = 2 ks + rr); the window
   // form's rows are the same for every k-tile (ROW3 plans only windows: computed once)
@@ -252,7 +257,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   auto step = [&](int k, int rs, int is) {
     wait_vmcnt<(NST - 2) * LPT>();
     ring_barrier();
-    const char* As = smem + rs * STAGE;
+    const char* As = ring + rs * STAGE;
     const char* Ps = As + A_BYTES;
     if (!ROW3) pixel_rows(kt_begin + k, pb);
     bf16x8 af[2][TR];
@@ -267,7 +272,7 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
         short tmp[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[ks][i] = __builtin_bit_cast(bf16x8, tmp);
       }
-    issue(kt_begin + k + NST - 1, is);  // the stage read at step k-1: all waves passed
+    issue(kt_begin + (k + NST - 1) * KG + kg, is);  // the stage read at step k-1: all waves passed
     // all 9 B fragments of a k-step are read before its 18 MFMAs, and the next k-step's reads are
     // issued while those run (two fragment buffers): one wave per SIMD has no other wave to hide
     // the LDS latency behind
@@ -316,17 +321,46 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
     }
   };
   if constexpr (ROW3) {
-    // stages as compile-time constants: every LDS address is a fixed per-lane offset + immediate
-    for (int k0 = 0; k0 < nk; k0 += NST) {
+    // stages as compile-time constants: every LDS address is a fixed per-lane offset + immediate.  Every
+    // group runs the same number of steps (a group past its last tile reads zeros): the barriers pair up
+    const int nloop = (nk + KG - 1) / KG;
+    for (int k0 = 0; k0 < nloop; k0 += NST) {
 #pragma unroll
       for (int u = 0; u < NST; ++u)
-        if (k0 + u < nk) step(k0 + u, u, (u + NST - 1) % NST);
+        if (k0 + u < nloop) step(k0 + u, u, (u + NST - 1) % NST);
     }
   } else {
     for (int k = 0; k < nk; ++k) step(k, k % NST, (k + NST - 1) % NST);
   }
   wait_vmcnt<0>();
-
+  if constexpr (KG > 1) {
+    // groups 1..KG-1 pass their accumulators through LDS (lane-contiguous: conflict-free); group 0 adds
+    // them in group order
+    constexpr int GF = NW * TR * NS * 16 * 64;  // floats per group
+    static_assert((KG - 1) * GF * 4 <= KG * NST * STAGE, "k-group exchange fits the rings");
+    float* xs = reinterpret_cast<float*>(smem);
+    ring_barrier();  // every wave's last fragment reads are done
+    if (kg > 0) {
+      float* xg = xs + (kg - 1) * GF;
+#pragma unroll
+      for (int i = 0; i < TR; ++i)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) xg[(((wid * TR + i) * NS + s) * 16 + v) * 64 + lane] = acc[i][s][v];
+    }
+    __syncthreads();
+    if (kg > 0) return;
+    for (int g2 = 0; g2 < KG - 1; ++g2) {
+      const float* xg = xs + g2 * GF;
+#pragma unroll
+      for (int i = 0; i < TR; ++i)
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[i][s][v] += xg[(((wid * TR + i) * NS + s) * 16 + v) * 64 + lane];
+    }
+  }
   // ---- epilogue: DW[m][tap][c] (slab: this split's partial, plain stores; else fp32 atomics) ----
   const int ldw = 9 * a.C;
   float* dst = a.slab ? a.slab + (size_t)split * a.K * ldw : a.dw;
@@ -362,17 +396,17 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 // (pass 2 runs over the group heads: step = per_group of pass 1)
 __global__ __launch_bounds__(256) void wgrad_halo_reduce_kernel(float* __restrict__ slab, int count, int step,
                                                                 int per_group, long long n, float* __restrict__ dw) {
-  const long long i = (blockIdx.x * 256LL + threadIdx.x) * 4;
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= n) return;
   const int s0 = blockIdx.y * per_group, s1 = min(count, s0 + per_group);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   int s = s0;
-  for (; s + 4 <= s1; s += 4) {  // four loads in flight, added in entry order
-    f32x4 v[4];
+  for (; s + 8 <= s1; s += 8) {  // eight loads in flight, added in entry order
+    f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(slab + (size_t)(s + u) * step * n + i);
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(slab + (size_t)(s + u) * step * n + i);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc += v[u];
+    for (int u = 0; u < 8; ++u) acc += v[u];
   }
   for (; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(slab + (size_t)s * step * n + i);
   if (gridDim.y == 1) {

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
     ap.add_argument("--wgrad-halo", default="3", help="comma list of avt_set_wgrad_halo values to sweep")
+    ap.add_argument("--row3-kg", default="1", help="comma list of avt_set_wgrad_row3 k-group values to sweep")
     ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
     ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
@@ -187,9 +188,11 @@ def main():
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
                 tot[("dgrad", v)] = tot.get(("dgrad", v), 0) + ms
             if "wgrad" in kinds and v == 1:
-                for hv, big in [(int(h), int(t)) for h in args.wgrad_halo.split(",")
-                                for t in args.wgrad_tiles.split(",")]:
+                for hv, big, kgv in [(int(h), int(t), int(g)) for h in args.wgrad_halo.split(",")
+                                     for t in args.wgrad_tiles.split(",") for g in args.row3_kg.split(",")]:
                     call("avt_set_wgrad_halo", hv)
+                    if args.row3_kg != "1":
+                        call("avt_set_wgrad_row3", kgv, -1)
                     call("avt_set_wgrad_tiles", big)
                     for nstp in args.wgrad_nst.split(";"):
                       if nstp != "4,3":  # (the default: also runs on a library without the setter)
@@ -201,8 +204,8 @@ def main():
                           ws = torch.empty(max(1, wsb), device=dev, dtype=torch.uint8)
                           ms = timeit(lambda: call("avt_conv2d_wgrad", P(x), P(dy), P(dw), N, H, W, C, C, K, R, R, st,
                                                    pad, P(ws), wsb if args.slab else 0, S()))
-                          line += f" wgrad[h{hv},t{big},{tb},{mk},n{nstp}] {flops / ms / 1e9:6.0f}"
-                          key = f"wgrad_h{hv}_t{big}_{pol}_n{nstp}"
+                          line += f" wgrad[h{hv},t{big},g{kgv},{tb},{mk},n{nstp}] {flops / ms / 1e9:6.0f}"
+                          key = f"wgrad_h{hv}_t{big}_g{kgv}_{pol}_n{nstp}"
                           tot[(key, v)] = tot.get((key, v), 0) + ms
                 if args.wgrad_nst != "4,3":
                     call("avt_set_wgrad_nst", 4, 3)
