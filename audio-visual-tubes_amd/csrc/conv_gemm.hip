@@ -1495,7 +1495,8 @@ static int wgrad_halo_enabled() {
 struct WgradHaloPlan {
   bool ok;
   bool row3; // one filter row (3 taps) per block: WM x 2 waves of 64 x 96, strip of PR - 2 PW patch rows
-  int kg;    // ROW3, WM 1: k groups per block (KG 2-wave groups on interleaved k-tiles, one partial per block)
+  int kg;    // ROW3: k groups per block (KG groups of WM x 2 waves on interleaved k-tiles, one partial per block;
+             // WM 2: at most 2)
   int WM;    // 2: BM 128 (4 waves), 1: BM 64 (2 waves)
   int RW;    // output channels per wave: 64, or 32 (9-tap form, K = 64: 4 waves of 32 x 288, two per SIMD)
   WgradHaloArgs a;
@@ -1531,8 +1532,8 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   const int ncols = pl.row3 ? 192 : 576;  // GEMM columns per block
   const int PRMAX = pl.row3 ? kRow3PrMax : (pl.WM == 2 && pl.RW == 64) ? 160 : 72;
   if (pl.row3 && getenv("AVT_ROW3_WM") && atoi(getenv("AVT_ROW3_WM")) == 1) pl.WM = 1;  // A/B: 64-row blocks at K >= 128
-  if (pl.row3 && pl.WM == 1) pl.kg = row3_kg();
-  const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 / pl.kg : 2) : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
+  if (pl.row3) pl.kg = pl.WM == 1 ? row3_kg() : (row3_kg() >= 2 ? 2 : 1);
+  const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 : 2) / pl.kg : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
   auto staged = [&](int pr, int pw) { return pl.row3 ? pr - 2 * pw : pr; };
   const double t_mfma = 2.0 * 32 * BM * ncols / (4 * 1024.0);
   auto cost = [&](long long tiles, int pr) {  // pr: staged patch rows
@@ -1598,7 +1599,9 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
   a.slab = slab;
   const int BM = pl.WM * pl.RW;
   const int grid = (a.K / BM) * (a.C / 64) * (pl.row3 ? 3 : 1) * a.splits;
-  if (pl.row3 && pl.WM == 2)
+  if (pl.row3 && pl.WM == 2 && pl.kg == 2)
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 4, kRow3PrMax, 64, true, 2>), dim3(grid), dim3(512), 0, st, a);
+  else if (pl.row3 && pl.WM == 2)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(256), 0, st, a);
   else if (pl.row3 && pl.kg == 4)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 4>), dim3(grid), dim3(512), 0, st, a);

@@ -207,19 +207,34 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
   };
-  for (int k = 0; k < nkt; ++k) {
+  auto step = [&](int k, int rs, int is) {  // rs: the stage read, is: the stage the DMA issued here fills
     wait_vmcnt<(NST - 2) * LPT>();
     ring_barrier();
-    const char* As = smem + (k % NST) * STAGE;
+    const char* As = smem + rs * STAGE;
     const char* Bs = As + A_BYTES;
     load_frags(As, Bs, 0, 0);
-    issue(kt_begin + k + NST - 1, (k + NST - 1) % NST);
+    issue(kt_begin + k + NST - 1, is);
     // step 1's fragments are read while step 0 multiplies
     load_frags(As, Bs, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     mma(0);
     __builtin_amdgcn_sched_barrier(0);
     mma(1);
+  };
+#ifndef AVT_TN_ROLLED  // (A/B build flag: the rolled loop)
+  if (true) {
+#else
+  if (false) {
+#endif
+    // unrolled by the ring depth: the stages are compile-time constants, so every fragment address is
+    // a fixed per-lane register + immediate (no per-read address adds)
+    for (int k0 = 0; k0 < nkt; k0 += NST) {
+#pragma unroll
+      for (int u = 0; u < NST; ++u)
+        if (k0 + u < nkt) step(k0 + u, u, (u + NST - 1) % NST);
+    }
+  } else {
+    for (int k = 0; k < nkt; ++k) step(k, k % NST, (k + NST - 1) % NST);
   }
   wait_vmcnt<0>();
   if constexpr (KG > 1) {  // group 1's accumulators into group 0's, through the (now idle) rings
