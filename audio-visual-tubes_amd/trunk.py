@@ -21,6 +21,10 @@ STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
 # 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
 # reduce/apply passes of avt_bn_bwd (measured 1 % faster: DESIGN §6f)
 FUSE_BN_BWD = os.environ.get("AVT_FUSE_BN_BWD", "0") == "1"
+# timing diagnostic (WRONG results; bench.py refuses it, tools/step_time.py measures with it): conv2 reads the
+# raw conv1 output instead of h1 = relu(bn1(conv1)) -- the upper bound of what fusing bn1 + ReLU into conv2's
+# operand loads could save (the 16 h1 apply launches and their 2 x 1 GB/step of traffic at B = 128)
+DIAG_H1_SKIP = os.environ.get("AVT_DIAG_H1_SKIP", "0") == "1"
 
 
 def P(t: Optional[torch.Tensor]):
@@ -260,9 +264,12 @@ class Trunk:
             t = {"x": cur, "H": Hc, "W": Wc}
             c1, s1, Ho, Wo = self._conv_bn(cur, N, Hc, Wc, blk["conv1"], blk["bn1"], store, training)
             yield
-            h1 = torch.empty_like(c1)
-            call("avt_bn_apply", P(c1), P(s1[0]), P(s1[1]), None, None, None, P(h1), N * Ho * Wo, c1.shape[-1], 1,
-                 stream_ptr())
+            if DIAG_H1_SKIP:
+                h1 = c1
+            else:
+                h1 = torch.empty_like(c1)
+                call("avt_bn_apply", P(c1), P(s1[0]), P(s1[1]), None, None, None, P(h1), N * Ho * Wo, c1.shape[-1],
+                     1, stream_ptr())
             yield
             c2, s2, _, _ = self._conv_bn(h1, N, Ho, Wo, blk["conv2"], blk["bn2"], store, training)
             yield

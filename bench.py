@@ -71,7 +71,7 @@ ALG_BYTES_PER_CLIP = 80.8e6  # each conv's input and output once
 
 # environment knobs that make the library compute WRONG results (timing diagnostics); a bench run refuses them.
 # Every other AVT_* variable (A/B performance knobs) is recorded in the JSON line.
-WRONG_RESULT_KNOBS = ("AVT_DIAG_SKIP", "AVT_C64_DBG", "AVT_TN_DBG", "AVT_HALO_DBG")
+WRONG_RESULT_KNOBS = ("AVT_DIAG_SKIP", "AVT_C64_DBG", "AVT_TN_DBG", "AVT_HALO_DBG", "AVT_DIAG_H1_SKIP")
 
 
 def check_env():
