@@ -64,21 +64,11 @@ constexpr int halo_blocks_per_cu() {
   return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
-// v moved one lane across the wave (DPP wave_shl:1 -- lane l takes lane l+1 -- or wave_shr:1); the lane with
-// no source gets 0
-template <bool LEFT>
-__device__ __forceinline__ bf16x8 wave_shift1(bf16x8 v) {
-  u32x4 u = __builtin_bit_cast(u32x4, v);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) u[e] = (unsigned)__builtin_amdgcn_update_dpp(0, (int)u[e], LEFT ? 0x130 : 0x138, 0xf, 0xf, false);
-  return __builtin_bit_cast(bf16x8, u);
-}
-
 // PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop).  Bench-only
 // (tools/halo_bench.hip, profiles/r5_halo_bench_pref.txt): +1..6 % on the layer4 shapes with a 4-stage ring, -3..5 %
 // on layer2; libavt launches PREF = 0
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
-          int PREF = 0, bool SHIFT = false>
+          int PREF = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   // fragment geometry: FM x FN MFMA tiles of FR rows per wave, KS k-steps of KD per 64-channel tap
@@ -150,10 +140,6 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   //      lane's k chunk within a k-step: fhalf (lanes 32-63 take k 8..15) ----
   const int frow = lane & (FR - 1), fhalf = lane / FR;
   unsigned fmask[FM];
-  // SHIFT: lanes whose A fragment at the 2nd / 3rd tap of a filter row is NOT their neighbour's at the tap
-  // before (fwd: lane l+1, dgrad: lane l-1 -- consecutive pixels of one image row are consecutive patch
-  // rows): the last (fwd) / first (dgrad) pixel of an image row, the fragment's edge row, pixels past M
-  bool fixl[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int row = wm * (BM / WM) + i * FR + frow;
@@ -169,7 +155,6 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       mk |= (ok && y >= 0 && y < H && x >= 0 && x < W ? 1u : 0u) << t;
     }
     fmask[i] = mk;
-    fixl[i] = !ok || (MODE == MODE_FWD ? (ow == W - 1 || frow == FR - 1) : (ow == 0 || frow == 0));
   }
   // ---- per-lane A row address of every (tap, row block), relative to the patch buffer: masked taps read
   //      the buffer's zero rows at the bank position the real row would have; the fragment-chunk swizzle
@@ -239,7 +224,6 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
   bf16x8 af[2][FM], bfr[2][FN];
-  bf16x8 aprev[SHIFT ? BK / KD : 1][FM];  // SHIFT: the previous tap's A fragments of every k-step
   auto mma = [&](int buf) {
     if (HALO_DBG(8)) return;
 #pragma unroll
@@ -366,27 +350,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         if (!HALO_DBG(4)) ring_barrier();
         const char* Bs = smem + 2 * ABUF + stage * BSTAGE;
         auto load_frags = [&](int ks, int buf) {
-          if constexpr (SHIFT) {
-            // 2nd / 3rd tap of a filter row: the fragment is the previous tap's moved one lane (DPP wave shift,
-            // no LDS read), the lanes where that is not so read theirs (an exec-masked read)
 #pragma unroll
-            for (int i = 0; i < FM; ++i) {
-              bf16x8 v;
-              if (t % 3 != 0) {
-                v = wave_shift1<MODE == MODE_FWD>(aprev[ks][i]);
-                typedef const volatile __attribute__((address_space(3))) bf16x8 lds_vbf16x8;
-                if (fixl[i]) v = *(lds_vbf16x8*)(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
-              } else {
-                v = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
-              }
-              af[buf][i] = v;
-              aprev[ks][i] = v;
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < FM; ++i)
-              af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
-          }
+          for (int i = 0; i < FM; ++i)
+            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[t][i] ^ (unsigned)(ks << 5)));
 #pragma unroll
           for (int j = 0; j < FN; ++j) bfr[buf][j] = *reinterpret_cast<const bf16x8*>(Bs + boffs[j][ks]);
         };
