@@ -1459,7 +1459,7 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
       else if (pl.nst >= 6)
         hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 6>), grid, dim3(256), 0, st, pp);
       else
-        hipLaunchKernelGGL((conv_tn_pipe_kernel<2, 2, BM / 64, BN / 64, 4>), grid, dim3(256), 0, st, pp);
+        launch_tn_one<2, 2, BM / 64, BN / 64, 4, 1>(grid, pp, st);
     }
     return;
   }
@@ -1483,6 +1483,12 @@ static int g_row3_kg = -1;  // ROW3 k groups per block (1 or 2); -1: env AVT_ROW
 static int row3_kg() {
   if (g_row3_kg < 0) g_row3_kg = getenv("AVT_ROW3_KG") ? atoi(getenv("AVT_ROW3_KG")) : 2;
   return (g_row3_kg == 2 || g_row3_kg == 4) ? g_row3_kg : 1;
+}
+static int g_row3_pf = -1;  // ROW3 (KG 2): next tile's first fragments read behind the MFMAs (default: +3-4 %);
+                            // -1: env AVT_ROW3_PF
+static int row3_pf() {
+  if (g_row3_pf < 0) g_row3_pf = getenv("AVT_ROW3_PF") ? atoi(getenv("AVT_ROW3_PF")) : 1;
+  return g_row3_pf;
 }
 static int wgrad_halo_enabled() {
   if (g_wgrad_halo < 0) {
@@ -1605,6 +1611,8 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<2, 4, kRow3PrMax, 64, true>), dim3(grid), dim3(256), 0, st, a);
   else if (pl.row3 && pl.kg == 4)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 4>), dim3(grid), dim3(512), 0, st, a);
+  else if (pl.row3 && pl.kg == 2 && row3_pf())
+    hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 2, true>), dim3(grid), dim3(256), 0, st, a);
   else if (pl.row3 && pl.kg == 2)
     hipLaunchKernelGGL((conv_wgrad_halo_kernel<1, 4, kRow3PrMax, 64, true, 2>), dim3(grid), dim3(256), 0, st, a);
   else if (pl.row3)
@@ -1627,11 +1635,13 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
   }
 }
 
-extern "C" int avt_set_wgrad_row3(int kg, int min_kt) {
+extern "C" int avt_set_wgrad_row3(int kg, int min_kt, int pf) {
   AVT_REQUIRE(kg == -1 || kg == 1 || kg == 2 || kg == 4, "avt_set_wgrad_row3: kg=%d (1, 2 or 4)", kg);
   AVT_REQUIRE(min_kt == -1 || min_kt >= 1, "avt_set_wgrad_row3: min_kt=%d", min_kt);
+  AVT_REQUIRE(pf >= -1 && pf <= 1, "avt_set_wgrad_row3: pf=%d", pf);
   if (kg > 0) g_row3_kg = kg;
   if (min_kt > 0) g_row3_min_kt = min_kt;
+  if (pf >= 0) g_row3_pf = pf;
   return AVT_OK;
 }
 

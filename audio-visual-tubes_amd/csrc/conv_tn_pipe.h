@@ -221,20 +221,16 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
     __builtin_amdgcn_sched_barrier(0);
     mma(1);
   };
-#ifndef AVT_TN_ROLLED  // (A/B build flag: the rolled loop)
-  if (true) {
-#else
-  if (false) {
-#endif
+  {
+    // (reading the next tile's first fragments across the barrier, as the row-form wgrad does, was measured
+    // 3-6 % slower here: with a 4-stage ring it leaves one tile in flight)
     // unrolled by the ring depth: the stages are compile-time constants, so every fragment address is
-    // a fixed per-lane register + immediate (no per-read address adds)
+    // a fixed per-lane register + immediate (no per-read address adds; +0-2 % over the rolled loop)
     for (int k0 = 0; k0 < nkt; k0 += NST) {
 #pragma unroll
       for (int u = 0; u < NST; ++u)
         if (k0 + u < nkt) step(k0 + u, u, (u + NST - 1) % NST);
     }
-  } else {
-    for (int k = 0; k < nkt; ++k) step(k, k % NST, (k + NST - 1) % NST);
   }
   wait_vmcnt<0>();
   if constexpr (KG > 1) {  // group 1's accumulators into group 0's, through the (now idle) rings

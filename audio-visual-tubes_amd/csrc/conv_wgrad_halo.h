@@ -57,11 +57,12 @@ struct WgradHaloArgs {
 // SIMD -- two blocks per CU).  ROW3 = true (RW = 64): the block owns one filter row fr (3 taps) and stages only
 // the patch rows that row reads (the "strip": PR - 2 PW rows); each wave 64 output channels x 3 taps x one
 // 32-channel half = 6 accumulator tiles, 2 A + 3 B fragment reads per 6 MFMAs.  BM = RW * WM
-template <int WM, int NST, int PRMAX, int RW = 64, bool ROW3 = false, int KG = 1>
+template <int WM, int NST, int PRMAX, int RW = 64, bool ROW3 = false, int KG = 1, bool PF = false>
 __global__ __launch_bounds__(WM * 2 * KG * 64) __attribute__((amdgpu_waves_per_eu(RW == 64 && !ROW3 ? 1 : 2, RW == 64 && !ROW3 ? 1 : 2)))
 void conv_wgrad_halo_kernel(WgradHaloArgs a) {
   static_assert(!ROW3 || RW == 64, "ROW3 form: 64 rows per wave");
   static_assert(KG == 1 || ROW3, "k groups: ROW3 form only");
+  static_assert(!PF || (ROW3 && NST >= 4), "PF: ROW3 form, a 4+ stage ring");
   constexpr int NW = WM * 2, BM = WM * RW, TR = RW / 32;
   constexpr int NS = ROW3 ? 3 : 9;                 // column subtiles per wave
   constexpr int AROWB = BM * 2;                    // bytes per DY row (pixel)
@@ -320,7 +321,72 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  if constexpr (ROW3) {
+  if constexpr (PF) {
+    // PF: each step's wait + barrier also publish the NEXT tile, whose first k-step fragments are read
+    // behind this step's MFMAs -- a step's MFMAs start right after its barrier instead of one LDS round
+    // trip later (ROW3 has only 2 k-steps per barrier).  One tile fewer in flight on the DMA side.
+    auto load_a = [&](const char* As, int ks, bf16x8* dst) {
+#pragma unroll
+      for (int i = 0; i < TR; ++i) {
+        const int c = wm * RW + i * 32 + tr_col;
+        const char* a0 = As + (ks * 16 + tr_row) * AROWB + ((c >> 3) ^ a_sw) * 16 + (c & 7) * 2;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * AROWB));
+        dst[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    auto load_b = [&](const char* Ps, int ks, bf16x8* dst) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {  // ROW3: tap fr*3 + s, channel half hn, PW rows up (see step)
+        const int disp = -a.PW + (s - 1);
+        const int rlo = pb[2 * ks] + disp, rhi = pb[2 * ks + 1] + disp;
+        const int c = hn * 32 + tr_col;
+        const char* b0 = Ps + rlo * 128 + (((c >> 3) ^ tn_swz<128>(rlo)) << 4) + (c & 7) * 2;
+        const char* b1 = Ps + rhi * 128 + (((c >> 3) ^ tn_swz<128>(rhi)) << 4) + (c & 7) * 2;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b0));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(b1));
+        dst[s] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    bf16x8 a0n[TR], b0n[NS];  // k-step 0 fragments of the step about to run
+    const int nloop = (nk + KG - 1) / KG;
+    wait_vmcnt<(NST - 2) * LPT>();  // tile 0 (every wave's, after the barrier)
+    ring_barrier();
+    load_a(ring, 0, a0n);
+    load_b(ring + A_BYTES, 0, b0n);
+    auto step_pf = [&](int k, int rs, int is) {
+      wait_vmcnt<(NST - 3) * LPT>();  // tiles k and k+1
+      ring_barrier();
+      const char* As = ring + rs * STAGE;
+      bf16x8 a1[TR], b1[NS];
+      load_a(As, 1, a1);
+      issue(kt_begin + (k + NST - 1) * KG + kg, is);  // the stage read at step k-1 (and prefetched before)
+      load_b(As + A_BYTES, 1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < TR; ++i)
+          acc[i][s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0n[i], b0n[s], acc[i][s], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < TR; ++i)
+          acc[i][s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1[s], acc[i][s], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < nloop) {  // the next tile: published by this step's barrier
+        const char* An = ring + ((rs + 1) % NST) * STAGE;
+        load_a(An, 0, a0n);
+        load_b(An + A_BYTES, 0, b0n);
+      }
+    };
+    for (int k0 = 0; k0 < nloop; k0 += NST) {
+#pragma unroll
+      for (int u = 0; u < NST; ++u)
+        if (k0 + u < nloop) step_pf(k0 + u, u, (u + NST - 1) % NST);
+    }
+  } else if constexpr (ROW3) {
     // stages as compile-time constants: every LDS address is a fixed per-lane offset + immediate.  Every
     // group runs the same number of steps (a group past its last tile reads zeros): the barriers pair up
     const int nloop = (nk + KG - 1) / KG;

@@ -40,7 +40,7 @@ class ResNet(nn.Module):
     """base_models.ResNet(BasicBlock, [2,2,2,2], modal) on libavt.  Inside an AVENet its parameters are
     views of the parent's flat storage; constructed on its own it keeps a flat store of its own.
     ``forward(x)`` (base_models.py:195-213) returns the layer4 map [N,512,h,w] fp32 with gradients
-    into the parameters (not into x: the 7x7 stem's input gradient is not computed)."""
+    into the parameters, and into x when x requires grad (avt_conv_stem_dgrad)."""
 
     def __init__(self, modal: str):
         super().__init__()
@@ -233,6 +233,9 @@ class _AVENetFunction(torch.autograd.Function):
         out, tape = engine.forward(image, audio, training, layer_io=sink is not None)
         if sink is not None:
             sink.update(out)
+        if tape is not None:  # d(loss)/d(frames, spectrogram) through the 7x7 stems when the inputs require it
+            tape["img"]["want_dx"] = ctx.needs_input_grad[3]
+            tape["aud"]["want_dx"] = ctx.needs_input_grad[4]
         ctx.engine = engine
         ctx.tape = tape
         ctx.n_params = len(params)
@@ -251,10 +254,11 @@ class _AVENetFunction(torch.autograd.Function):
         dev = next(g for g in (glogits, gwA, gA, gPos, gNeg) if g is not None).device
         gflat = torch.zeros(flat.n_train, device=dev, dtype=torch.float32)
         engine.backward(ctx.tape, glogits, gflat, dwA=gwA, dA=gA, dPos=gPos, dNeg=gNeg)
+        gimg, gaud = ctx.tape["img"].get("dx"), ctx.tape["aud"].get("dx")
         ctx.tape = None
         views = flat.param_grad_views(gflat)
         grads = tuple(views.get(n) for n in flat.pnames[:nparams])
-        return (None,) * 5 + grads
+        return (None, None, None, gimg, gaud) + grads
 
 
 class AVENet(nn.Module):
@@ -355,7 +359,8 @@ class AVENet(nn.Module):
         hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
                   if m._forward_hooks]
         sink = {} if hooked else None
-        need_grad = torch.is_grad_enabled() and self.training and any(p.requires_grad for p in train_params)
+        need_grad = torch.is_grad_enabled() and self.training and (
+            image.requires_grad or audio.requires_grad or any(p.requires_grad for p in train_params))
         if need_grad:
             A, logits, wA, Pos, Neg = _AVENetFunction.apply(eng, True, sink, image, audio, *train_params)
         else:

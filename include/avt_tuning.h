@@ -70,9 +70,10 @@ int avt_set_wgrad_tiles(int big);
  * block, 3 (default): form 2 for the K = 64 (layer-1) convs and the tap-gather kernel elsewhere -- or all
  * on the tap-gather one (0); env AVT_WGRAD_HALO.  Returns AVT_EINVAL outside 0..3 */
 int avt_set_wgrad_halo(int on);
-/* the one-filter-row form: k groups per 2-wave block pair (1, or 2: one partial tile per 4 waves; env
- * AVT_ROW3_KG, default 2) and the floor of k-tiles per split (env AVT_ROW3_MIN_KT, default 8); -1 keeps a value */
-int avt_set_wgrad_row3(int kg, int min_kt);
+/* the one-filter-row form: k groups per 2-wave block pair (1, 2 or 4; env AVT_ROW3_KG, default 2), the floor
+ * of k-tiles per split (env AVT_ROW3_MIN_KT, default 8), and (two k groups) the next tile's first fragments
+ * read behind the current tile's MFMAs (1, env AVT_ROW3_PF, default) or after its barrier (0); -1 keeps a value */
+int avt_set_wgrad_row3(int kg, int min_kt, int pf);
 /* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
  * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */
 int avt_set_stem_kernel(int on);

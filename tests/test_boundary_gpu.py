@@ -245,6 +245,52 @@ def test_standalone_trunks_forward_backward():
         assert params["conv1_flow.weight"].grad is None and params["fc.weight"].grad is None
 
 
+def test_avenet_input_gradients_vs_oracle():
+    """Frames and spectrogram that require grad (model.py:87-154 under the reference's autograd): image.grad and
+    audio.grad of CE + <A, rA> vs the fp64 oracle AVENet's, within 3x the deviation of the oracle with its trunks
+    in bf16 autocast; the parameter gradients are those of the same step without input gradients."""
+    img, aud = _tiny()
+    B = img.shape[0]
+    rA = 0.05 * torch.randn(B, 1, 4, 4, generator=torch.Generator().manual_seed(9))
+    zeros = torch.zeros(B, dtype=torch.long, device=DEV)
+    model = _model()
+    xi, xa = img.to(DEV).requires_grad_(True), aud.to(DEV).requires_grad_(True)
+    A, logits, _, _, _ = model(xi, xa)
+    (F.cross_entropy(logits, zeros) + (A * rA.to(DEV)).sum()).backward()
+    gw = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model2 = _model()
+    A2, logits2, _, _, _ = model2(img.to(DEV), aud.to(DEV))
+    (F.cross_entropy(logits2, zeros) + (A2 * rA.to(DEV)).sum()).backward()
+    for n, p_ in model2.named_parameters():  # the input gradients change nothing else
+        if p_.grad is not None:
+            assert torch.equal(p_.grad, gw[n]), n
+
+    def ref(sd, bf16):
+        ii, aa = (img.double(), aud.double()) if not bf16 else (img.clone(), aud.clone())
+        ii.requires_grad_(True)
+        aa.requires_grad_(True)
+        if bf16:
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                v = orc.resnet18_forward(sd, "imgnet.", ii, "vision", True)
+                a = orc.resnet18_forward(sd, "audnet.", aa, "audio", True)
+            v = F.normalize(v.float(), dim=1)
+            a = F.normalize(F.adaptive_max_pool2d(a.float(), 1).flatten(1), dim=1)
+            oA, olog, _, _, _ = orc.hardway_head(v, a)
+        else:
+            oA, olog, _, _, _ = orc.avenet_forward(dict(sd), ii, aa, None, training=True)
+        loss = orc.hardway_ce(olog) + (oA * rA.to(oA.dtype)).sum()
+        return torch.autograd.grad(loss, [ii, aa])
+
+    d64, dbf = ref(_sd64(), False), ref(orc.make_state(0), True)
+    for name, got, r64, rbf in (("image", xi.grad, d64[0], dbf[0]), ("audio", xa.grad, d64[1], dbf[1])):
+        e, eb = rel_err(got, r64), rel_err(rbf, r64)
+        c, cb = cosine(got, r64), cosine(rbf, r64)
+        print(f"{name}: dL/dx rel err {e:.3e} (bf16 reference {eb:.3e}), cosine {c:.4f} ({cb:.4f})")
+        assert got.shape == r64.shape and got.dtype == torch.float32
+        assert e <= max(2e-2, 3 * eb), (name, e, eb)
+        assert c >= min(0.98, 1 - 3 * (1 - cb)), (name, c, cb)
+
+
 def test_standalone_trunk_input_gradient():
     """A trunk whose input requires grad (base_models.py:195-210 under the reference's autograd, which returns
     d(loss)/dx through conv1 / conv1_a): x.grad of <map, R> vs the fp64 oracle trunk's, within 3x the deviation of

@@ -448,7 +448,7 @@ def wgrad(x, dy, dw, N, H, W, cp, creal, K, R, st, pad, slab=True):
 
 
 @pytest.mark.parametrize("nst", [(4, 3), (8, 5), (6, 4)], ids=["ring4", "ring8", "ring6"])
-@pytest.mark.parametrize("big", [1, 0, "halo", "halo3", "halo3k2", "halo3k4"])
+@pytest.mark.parametrize("big", [1, 0, "halo", "halo3", "halo3k2", "halo3k2np", "halo3k4"])
 @pytest.mark.parametrize("slab", [True, False])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_wgrad(case, slab, big, nst):
@@ -458,7 +458,7 @@ def test_conv_wgrad(case, slab, big, nst):
     the deep rings change the split plan too).  With the slab every form is run twice: bitwise equal."""
     if str(big).startswith("halo") and nst != (4, 3):
         pytest.skip("ring depth does not apply to the halo wgrad")
-    hv = {"halo": 1, "halo3": 2, "halo3k2": 2, "halo3k4": 2}.get(big, 0)
+    hv = {"halo": 1, "halo3": 2, "halo3k2": 2, "halo3k2np": 2, "halo3k4": 2}.get(big, 0)
     N, H, W, C, K, R, st, pad = case
     Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
     x = _rand_act(N, H, W, C, 8).relu()
@@ -468,7 +468,8 @@ def test_conv_wgrad(case, slab, big, nst):
     try:
         call("avt_set_wgrad_tiles", 1 if hv else big)
         call("avt_set_wgrad_halo", hv)
-        call("avt_set_wgrad_row3", {"halo3k2": 2, "halo3k4": 4}.get(big, 1), -1)
+        call("avt_set_wgrad_row3", {"halo3k2": 2, "halo3k2np": 2, "halo3k4": 4}.get(big, 1), -1,
+             0 if big == "halo3k2np" else 1)
         call("avt_set_wgrad_nst", *nst)
         xd, dyd = x.to(DEV), dy.to(DEV)
         wgrad(xd, dyd, dw, N, H, W, C, C, K, R, st, pad, slab)
@@ -477,7 +478,7 @@ def test_conv_wgrad(case, slab, big, nst):
     finally:
         call("avt_set_wgrad_tiles", 1)
         call("avt_set_wgrad_halo", 3)
-        call("avt_set_wgrad_row3", 1, -1)
+        call("avt_set_wgrad_row3", 2, -1, 1)
         call("avt_set_wgrad_nst", 4, 3)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)

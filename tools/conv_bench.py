@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--nt128", default="", help="comma list of avt_set_nt128_config values to sweep")
     ap.add_argument("--slab", type=int, default=1, help="wgrad split-K through a slab (1) or atomics (0)")
     ap.add_argument("--wgrad-halo", default="3", help="comma list of avt_set_wgrad_halo values to sweep")
-    ap.add_argument("--row3-kg", default="1", help="comma list of avt_set_wgrad_row3 k-group values to sweep")
+    ap.add_argument("--row3-kg", default="2", help="comma list of avt_set_wgrad_row3 k-group values to sweep")
     ap.add_argument("--halo", default="", help="comma list of avt_set_halo values to sweep (fwd/dgrad)")
     ap.add_argument("--small", default="", help="comma list of avt_set_small_tiles values to sweep (fwd/dgrad)")
     ap.add_argument("--stages", default="", help="';'-separated nst128,nst64 pairs of avt_set_halo_stages to sweep")
@@ -191,8 +191,8 @@ def main():
                 for hv, big, kgv in [(int(h), int(t), int(g)) for h in args.wgrad_halo.split(",")
                                      for t in args.wgrad_tiles.split(",") for g in args.row3_kg.split(",")]:
                     call("avt_set_wgrad_halo", hv)
-                    if args.row3_kg != "1":
-                        call("avt_set_wgrad_row3", kgv, -1)
+                    if args.row3_kg != "2":
+                        call("avt_set_wgrad_row3", kgv, -1, -1)
                     call("avt_set_wgrad_tiles", big)
                     for nstp in args.wgrad_nst.split(";"):
                       if nstp != "4,3":  # (the default: also runs on a library without the setter)
