@@ -32,10 +32,14 @@ def main():
             step.capture(*inputs)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         loss = step.step(*inputs)
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    print(f"host time per step() call (graph replay issue): {host * 1e3 / args.steps:.3f} ms", flush=True)
     knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("AVT_"))
     print(f"B={args.batch} {ms:.3f} ms/step {args.batch * 1e3 / ms:.1f} clips/s loss {float(loss.flatten()[0]):.4f} "
           f"[{knobs}]", flush=True)
