@@ -55,6 +55,15 @@ __device__ __forceinline__ void ring_barrier() {
 // PREVIOUS M0 -- land on the previous instruction's LDS slot -- on some waves of some launches: run-to-run
 // differences of a few launches in hundreds (the small-tile halo dgrad at 32 clips,
 // test_small_grid_conv_repeatable / tools/diag.py rep), which no tolerance check of the results can see.
+// lds_addr: the LDS byte address itself (an integer computed once from a shared-array base: converting a generic
+// pointer per call costs a null check, 2 scalar instructions)
+__device__ __forceinline__ void buf_lds16_at(__amdgpu_buffer_rsrc_t rs, unsigned lds_addr, unsigned voff) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff),
+               "s"(rs)
+               : "memory");
+}
+
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
   const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff),

@@ -121,14 +121,17 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
   }
   const unsigned a_step = 32u * (unsigned)(p.Mg * 2);
 
+  // the ring's LDS byte address as an integer, converted once (a generic-to-LDS pointer conversion per DMA costs a
+  // null check: 2 scalar instructions)
+  const unsigned smem_lds = (unsigned)(size_t)(lds_void_t*)smem;
   auto issue = [&](int kt, int stage) {  // tiles are issued in order; kt past the end is a dummy
-    char* As = smem + stage * STAGE;
-    char* Bs = As + A_BYTES;
+    const unsigned As = smem_lds + (unsigned)(stage * STAGE);
+    const unsigned Bs = As + A_BYTES;
     const bool live = kt < kt_end;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const bool ok = live && a_pix[i] < p.Kred;
-      buf_lds16(rsa, As + (wid * AI + i) * 1024, ok ? a_off[i] : kOOB);
+      buf_lds16_at(rsa, As + (unsigned)((wid * AI + i) * 1024), ok ? a_off[i] : kOOB);
       a_off[i] += a_step;
       a_pix[i] += 32;
     }
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
           live && b_colok[i] && b_pix[i] < p.Kred && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
       const unsigned off = b_nb[i] + __umul24((unsigned)y, rowB) + __umul24((unsigned)x, pixB) + cB[i];
       const unsigned m = 0u - (unsigned)ok;  // branch-free select
-      buf_lds16(rsb, Bs + (wid * BI + i) * 1024, (off & m) | (kOOB & ~m));
+      buf_lds16_at(rsb, Bs + (unsigned)((wid * BI + i) * 1024), (off & m) | (kOOB & ~m));
       b_pix[i] += 32;
       b_ow[i] += step_ow;
       b_oh[i] += step_oh;

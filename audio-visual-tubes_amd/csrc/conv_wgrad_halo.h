@@ -164,29 +164,56 @@ void conv_wgrad_halo_kernel(WgradHaloArgs a) {
 #pragma unroll
   for (int i = 0; i < PIW; ++i) p_lo[i] = (p_dy[i] * W + p_dx[i]) * a.C * 2 + (int)p_colB[i];
 
+  // ROW3: LDS byte addresses as integers; p_dy3 folds the lane's "past the patch" flag into its row (out of any image)
+  const unsigned ring_lds = (unsigned)(size_t)(lds_void_t*)ring, junk_lds = (unsigned)(size_t)(lds_void_t*)junk;
+  int p_dy3[PIW];
+#pragma unroll
+  for (int i = 0; i < PIW; ++i) p_dy3[i] = p_in[i] ? p_dy[i] : (1 << 20);
+  // ROW3: the issue cursor -- image, band and window column of the next tile to issue (tiles go out in order,
+  // KG apart): advanced with scalar adds, not two magic divisions per tile (the scalar instruction stream, one
+  // per CU, was ~7 per MFMA)
+  int cur_n = 0, cur_band = 0, cur_wc = 0;
+  const int bands = ROW3 ? a.tiles_img / a.wcols : 1;
+  if constexpr (ROW3) {
+    const int kt0 = kt_begin + kg;
+    cur_n = (int)magic_div((unsigned)kt0, a.div_tiles);
+    const int ti = kt0 - cur_n * a.tiles_img;
+    cur_band = (int)magic_div((unsigned)ti, a.div_wcols);
+    cur_wc = ti - cur_band * a.wcols;
+  }
   auto issue = [&](int kt, int stage) {
     char* As = ring + stage * STAGE;
     char* Ps = As + A_BYTES;
     const bool live = kt < kt_end;
-    const Tile t = tile_of(live ? kt : kt_begin);
     if constexpr (ROW3) {
-      const unsigned abase = (unsigned)(((t.n * H + t.y0) * W + t.x0) * a.K * 2);
-      const int py0 = t.yo + fr, hy = H - t.y0, wx = W - t.x0;
-      const int pbase = ((t.n * H + py0) * W + t.xo) * a.C * 2;
+      const int y0 = cur_band * a.R, x0 = cur_wc * a.CW;
+      const unsigned abase = (unsigned)(((cur_n * H + y0) * W + x0) * a.K * 2);
+      // a tile past the split's end: every bound fails (no per-load `live` term)
+      const int py0 = live ? y0 - 1 + fr : H, hy = live ? H - y0 : 0, wx = W - x0, xo = x0 - 1;
+      const int pbase = ((cur_n * H + py0) * W + xo) * a.C * 2;
+      const unsigned sa = ring_lds + (unsigned)(stage * STAGE);
+      cur_wc += KG;  // the next tile of this group (past the split's end: bases unused, the loads are out of range)
+      while (cur_wc >= a.wcols) {
+        cur_wc -= a.wcols;
+        if (++cur_band == bands) {
+          cur_band = 0;
+          ++cur_n;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        const bool ok = live && a_ky[i] < hy && a_kx[i] < wx;
-        buf_lds16(rs_dy, As + (wid * AI + i) * 1024, ok ? abase + a_lo[i] : kOOB);
+        const bool ok = a_ky[i] < hy && a_kx[i] < wx;
+        buf_lds16_at(rs_dy, sa + (unsigned)((wid * AI + i) * 1024), ok ? abase + a_lo[i] : kOOB);
       }
 #pragma unroll
       for (int i = 0; i < PIW; ++i) {
         const int q = i * NW + wid;
-        const bool pok = live && p_in[i] && (unsigned)(py0 + p_dy[i]) < (unsigned)H &&
-                         (unsigned)(t.xo + p_dx[i]) < (unsigned)W;
-        buf_lds16(rs_x, q < PINSTR ? Ps + q * 1024 : junk, pok ? (unsigned)(pbase + p_lo[i]) : kOOB);
+        const bool pok = (unsigned)(py0 + p_dy3[i]) < (unsigned)H && (unsigned)(xo + p_dx[i]) < (unsigned)W;
+        buf_lds16_at(rs_x, q < PINSTR ? sa + (unsigned)(A_BYTES + q * 1024) : junk_lds, pok ? (unsigned)(pbase + p_lo[i]) : kOOB);
       }
       return;
     }
+    const Tile t = tile_of(live ? kt : kt_begin);
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       int y, x;
