@@ -87,7 +87,7 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
   const unsigned imgB = (unsigned)(p.H * p.W * p.Cp * 2);
   const int step_oh = 32 / p.Q, step_ow = 32 - (32 / p.Q) * p.Q;
   const bool tiny = p.P * p.Q < 32;
-  int b_pix[BI], b_oh[BI], b_ow[BI], y_off[BI], x_off[BI];
+  int b_oh[BI], b_ow[BI], y_off[BI], x_off[BI];
   unsigned b_nb[BI], cB[BI];
   bool b_colok[BI];
 #pragma unroll
@@ -99,25 +99,22 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
     const int b_rr = rs / p.S, b_ss = rs - b_rr * p.S;
     b_colok[i] = col < p.R * p.S * p.Cp;
     y_off[i] = b_rr - p.pad;
-    x_off[i] = b_ss - p.pad;
+    x_off[i] = b_colok[i] ? b_ss - p.pad : (1 << 20);  // a column past R*S*C: always out of the image
     cB[i] = (unsigned)(b_c * 2);
     const int pix = kt_begin * 32 + row;
     const unsigned n = magic_div((unsigned)pix, pp.div_pq);
     const unsigned rem = (unsigned)pix - n * (unsigned)(p.P * p.Q);
     const unsigned oh = magic_div(rem, pp.div_q);
-    b_pix[i] = pix;
     b_oh[i] = (int)oh;
     b_ow[i] = (int)(rem - oh * (unsigned)p.Q);
     b_nb[i] = n * imgB;
   }
   unsigned a_off[AI];
-  int a_pix[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int row = (wid * AI + i) * A_RPI + a_r;
     const unsigned a_coff = (unsigned)((m0 + (a_pc ^ tn_swz<AROWB>(row)) * 8) * 2);
-    a_pix[i] = kt_begin * 32 + row;
-    a_off[i] = (unsigned)a_pix[i] * (unsigned)(p.Mg * 2) + a_coff;
+    a_off[i] = (unsigned)(kt_begin * 32 + row) * (unsigned)(p.Mg * 2) + a_coff;
   }
   const unsigned a_step = 32u * (unsigned)(p.Mg * 2);
 
@@ -128,37 +125,37 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
     const unsigned As = smem_lds + (unsigned)(stage * STAGE);
     const unsigned Bs = As + A_BYTES;
     const bool live = kt < kt_end;
+    // pixels past the batch (the last tile) need no test: their DY rows and image offsets lie past the end of
+    // the buffers, whose loads return zeros; a dead tile fails the row bound (H -> 0)
+    const unsigned Hl = live ? (unsigned)p.H : 0u;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
-      const bool ok = live && a_pix[i] < p.Kred;
-      buf_lds16_at(rsa, As + (unsigned)((wid * AI + i) * 1024), ok ? a_off[i] : kOOB);
+      buf_lds16_at(rsa, As + (unsigned)((wid * AI + i) * 1024), live ? a_off[i] : kOOB);
       a_off[i] += a_step;
-      a_pix[i] += 32;
     }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int y = (b_oh[i] << sh) + y_off[i], x = (b_ow[i] << sh) + x_off[i];
-      const bool ok =
-          live && b_colok[i] && b_pix[i] < p.Kred && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+      const bool ok = (unsigned)y < Hl && (unsigned)x < (unsigned)p.W;
       const unsigned off = b_nb[i] + __umul24((unsigned)y, rowB) + __umul24((unsigned)x, pixB) + cB[i];
-      const unsigned m = 0u - (unsigned)ok;  // branch-free select
-      buf_lds16_at(rsb, Bs + (unsigned)((wid * BI + i) * 1024), (off & m) | (kOOB & ~m));
-      b_pix[i] += 32;
-      b_ow[i] += step_ow;
-      b_oh[i] += step_oh;
-      if (b_ow[i] >= p.Q) {
-        b_ow[i] -= p.Q;
-        b_oh[i] += 1;
+      buf_lds16_at(rsb, Bs + (unsigned)((wid * BI + i) * 1024), ok ? off : kOOB);
+      // advance 32 pixels, branch-free (selects, no exec-mask branches: the scalar stream is one per CU)
+      int ow = b_ow[i] + step_ow, oh = b_oh[i] + step_oh;
+      const bool wr = ow >= p.Q;
+      ow = wr ? ow - p.Q : ow;
+      oh = wr ? oh + 1 : oh;
+      if (!tiny) {
+        const bool nx = oh >= p.P;  // next image
+        b_oh[i] = nx ? oh - p.P : oh;
+        b_nb[i] = nx ? b_nb[i] + imgB : b_nb[i];
+      } else {  // images of fewer than 32 pixels: several per tile (uniform branch)
+        while (oh >= p.P) {
+          oh -= p.P;
+          b_nb[i] += imgB;
+        }
+        b_oh[i] = oh;
       }
-      if (b_oh[i] >= p.P) {  // next image (more than once only for images of fewer than 32 pixels)
-        b_oh[i] -= p.P;
-        b_nb[i] += imgB;
-        if (tiny)
-          while (b_oh[i] >= p.P) {
-            b_oh[i] -= p.P;
-            b_nb[i] += imgB;
-          }
-      }
+      b_ow[i] = ow;
     }
   };
 
