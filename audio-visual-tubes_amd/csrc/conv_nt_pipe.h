@@ -65,7 +65,9 @@ __device__ __forceinline__ void buf_lds16_at(__amdgpu_buffer_rsrc_t rs, unsigned
 }
 
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
-  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave_base);
+  // the low 32 bits of a generic address into the LDS aperture are the LDS address (the aperture base is the high
+  // word): a truncation, where a cast to the LDS address space would add a null check per load
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)lds_wave_base);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds), "v"(voff),
                "s"(rs)
                : "memory");
