@@ -655,10 +655,19 @@ extern "C" int avt_set_wgrad_nst(int nst, int nst_big) {
 static inline int conv_out(int in, int k, int st, int pad) { return (in + 2 * pad - k) / st + 1; }
 
 template <int MODE, int WM, int WN, int TM, int TN, int NST, int BK>
-static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgsV& ta, hipStream_t st) {
+static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgsV& ta0, hipStream_t st) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN);
   if (grid <= 0) return;
+  NTPipeArgsV ta = ta0;  // the output grid's row divisors (per parity class for a multi-class dgrad)
+  ta.div_hw = make_magic((unsigned)(p.OH * p.OW));
+  ta.div_ow = make_magic((unsigned)p.OW);
+  for (int k = 0; k < 4; ++k) {
+    const int ph = (ta.cls_meta[k] >> 8) & 1, pw = (ta.cls_meta[k] >> 9) & 1;
+    const int oh = (ta.OHf - ph + 1) >> 1, ow = (ta.OWf - pw + 1) >> 1;
+    ta.cdiv_hw[k] = make_magic((unsigned)(oh > 0 && ow > 0 ? oh * ow : 1));
+    ta.cdiv_ow[k] = make_magic((unsigned)(ow > 0 ? ow : 1));
+  }
   if (p.IT > 1 || p.OT > 1 || ta.ntaps > 32) {  // Conv3d / the folded 49-tap video stem
     if constexpr (MODE == MODE_FWD)
       hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK, true>), dim3(grid), dim3(WM * WN * 64), 0,

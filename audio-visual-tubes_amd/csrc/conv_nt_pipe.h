@@ -90,6 +90,9 @@ struct NTPipeArgsT {
   // are tap_*[first tap ..]); class k's grid is ((OHf - ph + 1) / 2) x ((OWf - pw + 1) / 2) per sample.
   int ncls, batch;
   int cls_start[4], cls_meta[4];
+  // row -> (n, oh, ow) divisors of the output grid (ncls > 1: per class k), set by launch_pipe_one: the
+  // prologue's integer divisions were most of the short-K (1x1, strided) launches' instruction stream
+  MagicDiv div_hw, div_ow, cdiv_hw[4], cdiv_ow[4];
 };
 typedef NTPipeArgsT<9> NTPipeArgs;          // Conv2d (3x3 and 1x1)
 typedef NTPipeArgsT<kMaxTaps> NTPipeArgsV;  // Conv3d 3x3x3 and the folded 7x7 video stem
@@ -116,7 +119,11 @@ inline NTPipeArgs narrow_args(const NTPipeArgsV& v) {
   for (int k = 0; k < 4; ++k) {
     a.cls_start[k] = v.cls_start[k];
     a.cls_meta[k] = v.cls_meta[k];
+    a.cdiv_hw[k] = v.cdiv_hw[k];
+    a.cdiv_ow[k] = v.cdiv_ow[k];
   }
+  a.div_hw = v.div_hw;
+  a.div_ow = v.div_ow;
   return a;
 }
 
@@ -160,6 +167,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
   const int wm = wid / WN, wn = wid % WN;
   const int nnt = p.Ng / BN;
   int bid, ntaps = ta.ntaps, tb = 0, cph = ta.ph, cpw = ta.pw;
+  MagicDiv dhw = ta.div_hw, dow = ta.div_ow;
   if (!VID && MODE == MODE_DGRAD && ta.ncls > 1) {  // block-uniform: this block's parity class
     int k = 0;
 #pragma unroll
@@ -173,6 +181,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     p.OH = (ta.OHf - cph + 1) >> 1;
     p.OW = (ta.OWf - cpw + 1) >> 1;
     p.M = ta.batch * p.OH * p.OW;
+    dhw = ta.cdiv_hw[k];
+    dow = ta.cdiv_ow[k];
     bid = (int)blockIdx.x - ta.cls_start[k];  // heavy classes first in dispatch order; no XCD remap
   } else {
     bid = xcd_remap(blockIdx.x, gridDim.x);
@@ -203,11 +213,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
       ot = rem0 / hw;  // temporal stride 1: the row origin's t is ot
       rem = rem0 - ot * hw;
     } else {
-      n = mm / hw;
+      n = (int)magic_div((unsigned)mm, dhw);
       ot = 0;
       rem = mm - n * hw;
     }
-    const int oh = rem / p.OW, ow = rem - oh * p.OW;
+    const int oh = VID ? rem / p.OW : (int)magic_div((unsigned)rem, dow), ow = rem - oh * p.OW;
     int yb, xb;  // source coordinate of the row origin; tap t reads (yb + tap_dy[t], xb + tap_dx[t])
     if (MODE == MODE_FWD) {
       yb = oh * p.stride;
@@ -229,8 +239,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_nt_pipe_kernel(
     a_mask[i] = mask;
     if constexpr (VID)
       a_off0[i] = (unsigned)(((((long long)n * p.IT + ot) * p.IH + yb) * p.IW + xb) * p.IC + lc * 8) * 2u;
-    else
-      a_off0[i] = (unsigned)(((long long)n * p.IH * p.IW + (long long)yb * p.IW + xb) * p.IC + lc * 8) * 2u;
+    else  // 32-bit: the activation is < 2 GiB (act_bytes)
+      a_off0[i] = (unsigned)(((n * p.IH + yb) * p.IW + xb) * p.IC + lc * 8) * 2u;
   }
   unsigned b_off[BR];
 #pragma unroll
