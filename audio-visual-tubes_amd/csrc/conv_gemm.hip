@@ -460,7 +460,7 @@ static int stem_wgrad_enabled() {
   return g_stem_wgrad;
 }
 
-static int g_nt64_config = 1;   // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob)
+static int g_nt64_config = -1;  // tile config of the pipelined NT kernel for 64-wide GEMM N (A/B knob; -1 auto)
 static int g_nt128_config = -1; // ... and for GEMM N % 128 == 0 (-1: by GEMM M, see launch_nt)
 static int g_wgrad_blocks = 0;     // wgrad split-K: 0 = wave model (wgrad_plan), >0 = fixed block target
 static int g_wgrad_min_kt = 4;
@@ -596,7 +596,7 @@ extern "C" int avt_set_halo_stages(int nst128, int nst64) {
 }
 
 extern "C" int avt_set_nt64_config(int cfg) {
-  AVT_REQUIRE(cfg >= 0 && cfg <= 8, "set_nt64_config: cfg in 0..8");
+  AVT_REQUIRE(cfg >= -1 && cfg <= 8, "set_nt64_config: cfg in -1..8");
   g_nt64_config = cfg;
   return AVT_OK;
 }
@@ -1008,7 +1008,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
       return;
     }
   }
-  if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && g_nt64_config == 1 &&
+  if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && (g_nt64_config < 0 || g_nt64_config == 1) &&
       p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
     if (p.Ng % 128 == 0) {
       if (halo_eligible(p) && 64 + 2 * p.OW + 2 <= 104) {  // 64 x 128 halo tile
@@ -1052,7 +1052,11 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     if (p.Ng % 128 == 0) {
       // default: 256-row tiles (8 waves) where the GEMM is tall enough to fill the chip with them
       // (layer2, the stride-2 convs), 128 x 128 k64 tiles for the short layer3/4 GEMMs
-      const int cfg = g_nt128_config >= 0 ? g_nt128_config : (p.M >= 65536 ? 6 : 1);
+      // Conv3d (27 taps: 3x the K of a 3x3) keeps the 128 x 128 k64 tile unless K is short: on the R3D-18
+      // trunk (tools/conv3d_bench.py, profiles/r5_conv3d_tiles.txt) it is 10-15 % faster than the 256-row
+      // form on layer2/3's 3x3x3 convs; at layer2.0's K = 1728 the two are within 3 %
+      const bool vid = p.IT > 1 || p.OT > 1;
+      const int cfg = g_nt128_config >= 0 ? g_nt128_config : (p.M >= 65536 && (!vid || p.Kg < 3072) ? 6 : 1);
       switch (cfg) {
         case 1: launch_glds<MODE, 2, 2, 2, 2, 2, 64>(p, st); break;  // 128 x 128, k64, 2 stages
         case 2: launch_glds<MODE, 2, 2, 2, 2, 3, 64>(p, st); break;  // 128 x 128, k64, 3 stages
@@ -1063,7 +1067,9 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
         default: launch_glds<MODE, 2, 2, 2, 2>(p, st); break;        // 128 x 128, k32, 4 stages
       }
     } else {  // 64-wide N (layer1 / stem-fed convs)
-      switch (g_nt64_config) {
+      // auto (-1): 1, or 2 (4 stages) for a Conv3d -- R3D-18 layer1, profiles/r5_conv3d_tiles.txt: 548-579 us
+      // against 557-683 us per conv, ahead in every ordering measured
+      switch (g_nt64_config >= 0 ? g_nt64_config : (p.IT > 1 || p.OT > 1 ? 2 : 1)) {
         case 0: launch_glds<MODE, 4, 1, 2, 2, 4>(p, st); break;  // 256 x 64, 4 stages
         case 2: launch_glds<MODE, 2, 2, 2, 1, 4>(p, st); break;  // 128 x 64, 4 stages
         case 3: launch_glds<MODE, 4, 1, 2, 2, 2>(p, st); break;  // 256 x 64, 2 stages

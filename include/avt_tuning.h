@@ -20,8 +20,8 @@ int avt_set_conv_variant(int variant);
 /* weight-ring stages of the layer3/4 halo conv tiles: nst128 (128 x 128 tile) and nst64 (64 x 128
  * small-batch tile) in 2..5 (one block per CU from nst128 = 3 / nst64 = 4 on); all settings give bitwise-identical results (A/B knob) */
 int avt_set_halo_stages(int nst128, int nst64);
-/* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (0: 256x64/4 stages,
- * 1: 128x64/3 stages (default), 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
+/* tile config of the pipelined fwd/dgrad kernel when the GEMM N is 64 wide (-1 (default): 1, or 2 for a
+ * Conv3d; 0: 256x64/4 stages, 1: 128x64/3 stages, 2: 128x64/4 stages, 3: 256x64/2 stages, 4: 128x64 k64/3 stages,
  * 5: 256x64 k64/2 stages, 6: 128x64 k64/2 stages, 7: 256x64 8 waves k64/3, 8: 256x64 8 waves k64/2)
  * — an A/B knob */
 int avt_set_nt64_config(int cfg);
@@ -49,7 +49,8 @@ int avt_set_c64(int on);
  * classes (each with only the taps that reach it) as ONE launch, blocks of the classes with the most taps
  * dispatched first; 0: one launch per class.  The results are bitwise identical (same tap order). */
 int avt_set_s2_dgrad_one(int on);
-/* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default);
+/* ... and when the GEMM N is a multiple of 128 (-1: by GEMM M, 6 if M >= 65536 else 1 (default; a Conv3d
+ * with K >= 3072 always 1);
  * 0: 128x128 k32/4 stages, 1: 128x128 k64/2, 2: 128x128 k64/3, 3: 256x128 k32/3, 4: 256x128 k64/2,
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */
 int avt_set_nt128_config(int cfg);

@@ -195,7 +195,7 @@ def test_conv_variants_bitwise_equal(case):
                 assert torch.equal(dx, outs[0][1]), (knob, cfg)
     finally:
         call("avt_set_nt128_config", -1)
-        call("avt_set_nt64_config", 1)
+        call("avt_set_nt64_config", -1)
         call("avt_set_halo", 1)
 
 

@@ -92,6 +92,39 @@ def test_conv3d_fwd_and_bn_stats(case):
                                atol=1e-4 * var.max().item())
 
 
+@pytest.mark.parametrize("C,K", [(64, 64), (64, 128), (128, 128)])
+def test_conv3d_tile_configs(C, K):
+    """Conv3d at a GEMM M >= 65536 (where the tile choice depends on K) under every tile config the
+    planner picks from (launch_nt): bitwise-equal outputs (the same k order per element), checked against
+    torch on output frames 0-1."""
+    N, T, H, W = 1, 8, 96, 96
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, T, H, W, C, generator=g).relu().to(torch.bfloat16)
+    w = (torch.randn(K, C, 3, 3, 3, generator=g) * (2.0 / (K * 27)) ** 0.5).float()
+    wp = torch.empty(K, 27 * C, device=DEV, dtype=torch.bfloat16)
+    call("avt_pack_conv3d_weight", P(w.to(DEV)), P(wp), K, C, 3, 3, 3, 0, S())
+    xd = x.to(DEV)
+    knobs = [("avt_set_nt64_config", v) for v in (-1, 1, 0)] if K == 64 else \
+            [("avt_set_nt128_config", v) for v in (-1, 1, 6)]
+    outs = []
+    try:
+        for fn, v in knobs:
+            call(fn, v)
+            y = torch.empty(N, T, H, W, K, device=DEV, dtype=torch.bfloat16)
+            call("avt_conv3d_fwd", P(xd), P(wp), P(y), None, N, T, H, W, C, K, 3, 3, 3, 1, 1, 1, S())
+            outs.append(y)
+        torch.cuda.synchronize()
+    finally:
+        call("avt_set_nt64_config", -1)
+        call("avt_set_nt128_config", -1)
+    for (fn, v), o in zip(knobs[1:], outs[1:]):
+        assert torch.equal(o, outs[0]), (fn, v)
+    # output frames 0 and 1 read input frames 0-2 only
+    ref = F.conv3d(x[:, :3].float().permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).float(), padding=1)[:, :, :2]
+    err = rel_err(outs[0][:, :2], ref.permute(0, 2, 3, 4, 1))
+    assert err < 8e-3, err
+
+
 @pytest.mark.parametrize("shape", [(2, 4, 32, 32), (1, 16, 30, 22), (1, 3, 17, 9)])
 def test_video_stem_fold(shape):
     """Stem Conv3d(3,64,(7,7,7),s(1,2,2),p3) = im2col (temporal taps -> channels) + 7x7/s2 conv."""

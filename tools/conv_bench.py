@@ -160,7 +160,7 @@ def main():
                     ms = timeit(lambda: call("avt_conv2d_dgrad", P(dy), P(wt), P(dx), None, N, H, W, C, K, R, R, st,
                                              pad, S()))
                     line += f" nt64[{cfg}] dgrad {flops / ms / 1e9:6.0f}"
-            call("avt_set_nt64_config", 1)
+            call("avt_set_nt64_config", -1)
         if args.nt128 and K % 128 == 0 or args.nt128 and C % 128 == 0:
             for cfg in [int(s) for s in args.nt128.split(",")]:
                 call("avt_set_nt128_config", cfg)
