@@ -547,6 +547,32 @@ def test_bn_forward_train(shape):
     np.testing.assert_allclose(rvd.cpu().numpy(), rv64.numpy(), rtol=1e-4, atol=1e-5)
 
 
+def test_bn_finalize_tall():
+    """The forward finalize over 8200 tile slots (a GEMM of 2^20 rows: the tube step's 16-frame stem and
+    layer1 have ~12.5 k), against the fp64 statistics of the same rows."""
+    T, C = 8200, 64
+    g = torch.Generator().manual_seed(21)
+    rows = (torch.randn(T * 128, C, generator=g) * 1.3 + 0.4).to(torch.bfloat16).double()
+    blk = rows.view(T, 128, C)
+    s = blk.sum(1)
+    acc = torch.stack([s, ((blk - blk.mean(1, keepdim=True)) ** 2).sum(1), s * s / 128], dim=2)
+    hdr = torch.zeros(8, dtype=torch.float64)
+    hdr[0] = T
+    accd = torch.cat([hdr, acc.reshape(-1)]).to(DEV)
+    gamma = torch.ones(C, device=DEV)
+    beta = torch.zeros(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    stats = torch.empty(4, C, device=DEV)
+    call("avt_bn_finalize", P(accd), T * 128, C, P(gamma), P(beta), P(rm), P(rv), ctypes.c_float(0.1),
+         ctypes.c_float(1e-5), P(stats[0]), P(stats[1]), P(stats[2]), P(stats[3]), S())
+    torch.cuda.synchronize()
+    mean, var = rows.mean(0), rows.var(0, unbiased=False)
+    np.testing.assert_allclose(stats[2].cpu().double().numpy(), mean.numpy(), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(stats[3].cpu().double().numpy(), (1 / (var + 1e-5).sqrt()).numpy(), rtol=1e-6)
+    np.testing.assert_allclose(rv.cpu().double().numpy(), (0.9 + 0.1 * rows.var(0, unbiased=True)).numpy(),
+                               rtol=1e-6)
+
+
 @pytest.mark.parametrize("shape", [(2, 9, 11, 64), (4, 5, 7, 512), (3, 33, 38, 128)])
 @pytest.mark.parametrize("masked", [True, False])
 def test_bn_backward(shape, masked):
