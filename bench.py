@@ -261,6 +261,16 @@ def cpu_baseline(workload: str, budget_s: float = 20.0):
                       f"{n}; fwd_loss_clips_per_s: forward + CE only (configs[0]), median of {n_f}"}
 
 
+def eager_copy(step):
+    """A view of the train step (same buffers, optimizer, engine) whose step() launches every kernel eagerly.
+    Every captured form must be dropped -- world 1: _graph; world > 1: _seg_graphs (overlap schedule) or
+    _graph + _graph_opt -- or step() replays it and the conv profiler sees no launch."""
+    eager = type(step).__new__(type(step))
+    eager.__dict__.update(step.__dict__)
+    eager._graph = eager._graph_opt = eager._seg_graphs = None
+    return eager
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -296,9 +306,19 @@ def main():
     if args.gpus != world:  # before any GPU call: a mismatch would report the wrong n_gpus
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 as "
                  f"python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py --gpus {args.gpus}")
+    # Test-only overrides (tests/test_bench_dist_gpu.py), recorded in avt_env and "backend": the one-GPU box runs the
+    # world > 1 branch with every rank on cuda:0 over gloo, since RCCL needs one device per rank.
+    backend = os.environ.get("AVT_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        sys.exit(f"bench.py: AVT_BENCH_BACKEND={backend!r}: expected nccl or gloo")
+    if os.environ.get("AVT_BENCH_ONE_DEVICE", "0") not in ("", "0"):
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
 
     import avtubes  # noqa: F401
@@ -372,9 +392,7 @@ def main():
     loss_v = float(loss.flatten()[0])  # twoview: losses[0] = the combined loss
     # roofline of the conv family: HIP events on the launch stream around every conv launch of a
     # few eager steps of the same workload (kept out of the timed region above)
-    eager = type(step).__new__(type(step))
-    eager.__dict__.update(step.__dict__)
-    eager._graph = None
+    eager = eager_copy(step)
     conc = step.engine.concurrent
     step.engine.concurrent = False  # per-kernel durations of the conv launches, not of overlapped pairs
     with ConvProfiler() as prof:
@@ -383,6 +401,8 @@ def main():
         torch.cuda.synchronize()
     step.engine.concurrent = conc
     conv = prof.summary()
+    if args.prof_steps > 0 and not conv:
+        sys.exit("bench.py: the profiled eager steps launched no conv kernel (a captured graph was replayed?)")
     peaks = None if args.no_peaks else measure_peaks(dev)
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
@@ -431,6 +451,7 @@ def main():
             "data": DATA,
             "config": {"workload": workload, "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": f"dp{world}"},
+            "backend": (backend if world > 1 else None),
             "roofline": {"bound": "mfma", "kernel": "conv implicit-GEMM (fwd+dgrad+wgrad)",
                          "achieved": round(achieved, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,

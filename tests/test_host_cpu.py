@@ -241,3 +241,31 @@ def test_bench_refuses_wrong_results_knobs(knob):
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "refusing" in (r.stderr + r.stdout) and knob in (r.stderr + r.stdout)
+
+
+def test_bench_eager_copy_drops_every_captured_form():
+    """bench.py's roofline profiles an eager copy of the train step.  At world > 1 the overlap schedule keeps its
+    capture in _seg_graphs (the non-overlap one in _graph + _graph_opt); a copy that kept either would replay it and
+    the profiler would see no conv launch (roofline.launches 0 at N > 1)."""
+    import importlib.util
+
+    import avtubes  # noqa: F401
+    from avt_amd.train import HardWayTrainStep
+
+    spec = importlib.util.spec_from_file_location("avt_bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    calls = []
+    for captured in ({"_graph": object(), "_graph_opt": None, "_seg_graphs": None},
+                     {"_graph": None, "_graph_opt": None, "_seg_graphs": [object(), object()]},
+                     {"_graph": object(), "_graph_opt": object(), "_seg_graphs": None}):
+        step = HardWayTrainStep.__new__(HardWayTrainStep)
+        step.__dict__.update(captured)
+        step._replay = lambda *a: calls.append("replay")
+        step._eager_step = lambda *a: calls.append("eager")
+        step.step()
+        eager = bench.eager_copy(step)
+        eager.step()
+        assert eager._replay is step._replay  # same state otherwise
+    assert calls == ["replay", "eager"] * 3, calls
