@@ -1549,10 +1549,10 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
     pl.WM = 2;
     pl.RW = 32;
   }
-  const int BM = pl.WM * pl.RW;
+  if (pl.row3 && getenv("AVT_ROW3_WM") && atoi(getenv("AVT_ROW3_WM")) == 1) pl.WM = 1;  // A/B: 64-row blocks at K >= 128
+  const int BM = pl.WM * pl.RW;  // after every WM override: the plan and the launch use the same block rows
   const int ncols = pl.row3 ? 192 : 576;  // GEMM columns per block
   const int PRMAX = pl.row3 ? kRow3PrMax : (pl.WM == 2 && pl.RW == 64) ? 160 : 72;
-  if (pl.row3 && getenv("AVT_ROW3_WM") && atoi(getenv("AVT_ROW3_WM")) == 1) pl.WM = 1;  // A/B: 64-row blocks at K >= 128
   if (pl.row3) pl.kg = pl.WM == 1 ? row3_kg() : (row3_kg() >= 2 ? 2 : 1);
   const int per_cu = pl.row3 ? (pl.WM == 1 ? 4 : 2) / pl.kg : (pl.WM == 2 && pl.RW == 64) ? 1 : 2;  // resident blocks per CU
   auto staged = [&](int pr, int pw) { return pl.row3 ? pr - 2 * pw : pr; };
@@ -1654,14 +1654,15 @@ extern "C" int avt_set_wgrad_row3(int kg, int min_kt, int pf) {
   AVT_REQUIRE(kg == -1 || kg == 1 || kg == 2 || kg == 4, "avt_set_wgrad_row3: kg=%d (1, 2 or 4)", kg);
   AVT_REQUIRE(min_kt == -1 || min_kt >= 1, "avt_set_wgrad_row3: min_kt=%d", min_kt);
   AVT_REQUIRE(pf >= -1 && pf <= 1, "avt_set_wgrad_row3: pf=%d", pf);
-  if (kg > 0) g_row3_kg = kg;
-  if (min_kt > 0) g_row3_min_kt = min_kt;
-  if (pf >= 0) g_row3_pf = pf;
+  // -1 resets a value to its environment default (re-read on next use), as the sibling setters do
+  g_row3_kg = kg;
+  g_row3_min_kt = min_kt;
+  g_row3_pf = pf;
   return AVT_OK;
 }
 
 extern "C" int avt_set_wgrad_halo(int on) {
-  AVT_REQUIRE(on >= 0 && on <= 3, "avt_set_wgrad_halo: %d (0 off, 1 nine taps, 2 one filter row per block, 3 = 2 for K 64)", on);
+  AVT_REQUIRE(on >= -1 && on <= 3, "avt_set_wgrad_halo: %d (0 off, 1 nine taps, 2 one filter row per block, 3 = 2 for K 64, -1 env)", on);
   avt::g_wgrad_halo = on;
   return AVT_OK;
 }

@@ -359,6 +359,11 @@ class AVENet(nn.Module):
         hooked = [(n, m) for n, m in (("imgnet", self.imgnet.layer4), ("audnet", self.audnet.layer4))
                   if m._forward_hooks]
         sink = {} if hooked else None
+        if torch.is_grad_enabled() and not self.training and (image.requires_grad or audio.requires_grad):
+            # as ResNet.forward: an input gradient through eval-mode BatchNorm is not computed -- refuse here rather
+            # than return detached outputs whose backward() fails far from the cause
+            raise NotImplementedError("avt: gradients through an eval-mode AVENet are not computed (train-mode "
+                                      "BatchNorm only)")
         need_grad = torch.is_grad_enabled() and self.training and (
             image.requires_grad or audio.requires_grad or any(p.requires_grad for p in train_params))
         if need_grad:

@@ -192,8 +192,12 @@ class HardWayTrainStep:
     def capture(self, *inputs: torch.Tensor) -> None:
         """Record one step into HIP graph(s) (torch.cuda.CUDAGraph is hipGraph on ROCm) so that
         later steps are replays: no per-kernel host launch cost and no launch gaps between the
-        ~700 kernels of a step.  World 1: one graph (fwd + CE + bwd + Adam).  World > 1: the RCCL
-        collectives stay eager between two graphs (fwd+bwd, then Adam).  ``image``/``audio``
+        ~700 kernels of a step.  World 1: one graph (fwd + CE + bwd + Adam).  World > 1, overlap schedule
+        (default): one graph per backward segment (fwd + layer4/3 backward of both trunks | layer2..stem), replayed
+        in order; between and after the replays the bucket all-reduces and their Adam updates stay eager
+        (_dp_boundary: a "hi" bucket's update on the Adam side stream behind its collective; _dp_finish: the "lo"
+        buckets, then the join).  World > 1 without overlap: fwd+bwd graph, the eager all-reduce, an Adam graph.
+        ``image``/``audio``
         become the static inputs; later steps copy theirs in unless they pass these tensors.
         Call after at least one eager step (the engine allocates its buffers lazily).  Capture
         records launches without running them, so it has no effect on the training state."""

@@ -25,6 +25,10 @@ FUSE_BN_BWD = os.environ.get("AVT_FUSE_BN_BWD", "0") == "1"
 # raw conv1 output instead of h1 = relu(bn1(conv1)) -- the upper bound of what fusing bn1 + ReLU into conv2's
 # operand loads could save (the 16 h1 apply launches and their 2 x 1 GB/step of traffic at B = 128)
 DIAG_H1_SKIP = os.environ.get("AVT_DIAG_H1_SKIP", "0") == "1"
+if DIAG_H1_SKIP and os.environ.get("AVT_DIAG_WRONG_RESULTS_OK", "0") != "1":
+    # a training run under this variable would silently train another network: it needs an explicit opt-in
+    raise RuntimeError("avt: AVT_DIAG_H1_SKIP=1 computes WRONG results (timing diagnostic); set "
+                       "AVT_DIAG_WRONG_RESULTS_OK=1 as well to run it (tools/step_time.py)")
 
 
 def P(t: Optional[torch.Tensor]):

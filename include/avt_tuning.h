@@ -69,11 +69,12 @@ int avt_set_wgrad_slab_max(int max_splits, int wave_cost);
 int avt_set_wgrad_tiles(int big);
 /* 3x3/s1 wgrads on the halo-reuse kernel -- 1: all 9 taps per block, 2: one filter row (3 taps) per
  * block, 3 (default): form 2 for the K = 64 (layer-1) convs and the tap-gather kernel elsewhere -- or all
- * on the tap-gather one (0); env AVT_WGRAD_HALO.  Returns AVT_EINVAL outside 0..3 */
+ * on the tap-gather one (0); -1: back to env AVT_WGRAD_HALO.  Returns AVT_EINVAL outside -1..3 */
 int avt_set_wgrad_halo(int on);
 /* the one-filter-row form: k groups per 2-wave block pair (1, 2 or 4; env AVT_ROW3_KG, default 2), the floor
  * of k-tiles per split (env AVT_ROW3_MIN_KT, default 8), and (two k groups) the next tile's first fragments
- * read behind the current tile's MFMAs (1, env AVT_ROW3_PF, default) or after its barrier (0); -1 keeps a value */
+ * read behind the current tile's MFMAs (1, env AVT_ROW3_PF, default) or after its barrier (0); -1 resets a value
+ * to its environment default */
 int avt_set_wgrad_row3(int kg, int min_kt, int pf);
 /* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
  * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */

@@ -169,3 +169,58 @@ def test_segment_graph_replay_matches_eager():
         g_rep, g_eag, buckets = _seg_vs_eager()
         for tag, (lo, hi) in buckets.items():
             assert torch.equal(g_rep[lo:hi], g_eag[lo:hi]), tag
+
+
+class _DelayedWork:
+    """A stand-in for an async RCCL work object: the 'collective' runs on its own stream behind a sleep kernel
+    and doubles the bucket (g + g: two ranks with the same shard); wait() is a stream-side wait, as RCCL's."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+
+def test_side_stream_adam_ordering_without_host_sync(monkeypatch):
+    """the world > 1 overlap schedule updates each "hi" bucket on the Adam side stream behind its
+    collective, and _dp_finish joins that stream into the current one.  With a collective that finishes late on
+    its own stream (sleep kernel), the weights read on the current stream right after step() -- no host sync --
+    must already be the DP update: Adam on (g + g) / 2 = the world-1 update, bit for bit.  Eager steps and
+    segment-graph replays."""
+    import avtubes  # noqa: F401
+    from avt_amd.train import HardWayTrainStep
+
+    dev = torch.device("cuda", 0)
+    comm = torch.cuda.Stream(device=dev)
+
+    def fake_all_reduce(t, op=None, group=None, async_op=False):
+        comm.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(comm):
+            torch.cuda._sleep(20_000_000)  # ~10 ms: far longer than the rest of the step's tail
+            t.mul_(2.0)
+            ev = torch.cuda.Event()
+            ev.record(comm)
+        w = _DelayedWork(ev)
+        if async_op:
+            return w
+        w.wait()
+
+    monkeypatch.setattr(dist, "all_reduce", fake_all_reduce)
+    img, aud = orc.make_image(2, 64).to(dev), orc.make_spectrogram(2, 65, 76).to(dev)
+    m = _model(dev)
+    step = HardWayTrainStep(m, lr=1e-4, weight_decay=1e-4)
+    step.world, step.overlap = 2, True  # one process, the world > 1 overlap schedule
+    ref_m = _model(dev)
+    ref = HardWayTrainStep(ref_m, lr=1e-4, weight_decay=1e-4)
+    for i in range(4):
+        if i == 2:
+            step.capture(img.clone(), aud.clone())
+        step.step(img, aud)
+        snap = m._flat.flat.clone()  # enqueued on the current stream right after step(): no host sync
+        ref._fwd_bwd(img, aud)
+        ref.opt.step(ref.grad * 2.0, grad_scale=0.5)
+        torch.cuda.synchronize()
+        assert torch.equal(snap, ref_m._flat.flat), f"step {i}: weights read before the side-stream Adam finished"
+    assert step._seg_graphs is not None and len(step._seg_graphs) == 2

@@ -269,3 +269,19 @@ def test_bench_eager_copy_drops_every_captured_form():
         eager.step()
         assert eager._replay is step._replay  # same state otherwise
     assert calls == ["replay", "eager"] * 3, calls
+
+
+def test_h1_skip_diagnostic_needs_opt_in():
+    """AVT_DIAG_H1_SKIP makes the trunks compute a different network (timing diagnostic): importing the library
+    under it fails unless AVT_DIAG_WRONG_RESULTS_OK=1 is set as well."""
+    import subprocess
+    import sys
+
+    code = "import avtubes; import avt_amd.trunk as t; print('H1', t.DIAG_H1_SKIP)"
+    env = {k: v for k, v in os.environ.items() if k != "AVT_DIAG_WRONG_RESULTS_OK"}
+    env["AVT_DIAG_H1_SKIP"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WRONG results" in r.stderr
+    env["AVT_DIAG_WRONG_RESULTS_OK"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "H1 True" in r.stdout, r.stderr

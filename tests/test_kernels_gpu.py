@@ -477,8 +477,8 @@ def test_conv_wgrad(case, slab, big, nst):
             wgrad(xd, dyd, dw2, N, H, W, C, C, K, R, st, pad, slab)
     finally:
         call("avt_set_wgrad_tiles", 1)
-        call("avt_set_wgrad_halo", 3)
-        call("avt_set_wgrad_row3", 2, -1, 1)
+        call("avt_set_wgrad_halo", -1)  # back to the environment defaults (AVT_WGRAD_HALO, AVT_ROW3_*)
+        call("avt_set_wgrad_row3", -1, -1, -1)
         call("avt_set_wgrad_nst", 4, 3)
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (K, C, R, R), dy.double().permute(0, 3, 1, 2),
                                       stride=st, padding=pad)

@@ -181,6 +181,21 @@ def test_eval_mode_uses_running_stats(golden_dir):
     assert int(model.state_dict()["imgnet.bn1.num_batches_tracked"]) == 0
 
 
+def test_eval_mode_input_gradient_refused():
+    """An input gradient through eval-mode BatchNorm is not computed: AVENet refuses it as the standalone ResNet
+    does, instead of returning detached outputs; without input gradients eval mode runs."""
+    img, aud = orc.make_image(2, 64).to(DEV), orc.make_spectrogram(2, 65, 76).to(DEV)
+    model = _model().eval()
+    with pytest.raises(NotImplementedError, match="eval-mode"):
+        model(img.clone().requires_grad_(), aud)
+    with pytest.raises(NotImplementedError, match="eval-mode"):
+        model(img, aud.clone().requires_grad_())
+    with pytest.raises(NotImplementedError, match="eval-mode"):
+        model.imgnet(img.clone().requires_grad_())
+    A = model(img, aud)[0]  # grad mode on, parameters require grad, inputs do not: the eval forward
+    assert not A.requires_grad and torch.isfinite(A).all()
+
+
 def test_train_step_is_deterministic():
     """two runs of the fused train step from the same weights on the same inputs give
     bitwise-equal losses, gradients, weights and BN running statistics -- no atomics in any reduction

@@ -211,7 +211,7 @@ def main():
                     call("avt_set_wgrad_nst", 4, 3)
                 call("avt_set_wgrad_policy", 0, 4)
                 call("avt_set_wgrad_tiles", 1)
-                call("avt_set_wgrad_halo", 3)
+                call("avt_set_wgrad_halo", -1)
         print(line + "  TFLOP/s", flush=True)
     call("avt_set_conv_variant", 1)
     print({f"{k}_v{v}": round(ms, 3) for (k, v), ms in tot.items()}, "ms total")

@@ -1,6 +1,6 @@
 """Step timer for timing DIAGNOSTICS that bench.py refuses (wrong-results knobs such as AVT_DIAG_H1_SKIP):
 the 1-frame train step on synthetic inputs, captured as bench.py does, K timed replays.  Prints one line.
-usage: AVT_DIAG_H1_SKIP=1 python tools/step_time.py --batch 128 --steps 20 --warmup 5"""
+usage: AVT_DIAG_H1_SKIP=1 AVT_DIAG_WRONG_RESULTS_OK=1 python tools/step_time.py --batch 128 --steps 20 --warmup 5"""
 import argparse
 import os
 import sys
