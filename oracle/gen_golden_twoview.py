@@ -22,7 +22,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import avenet_oracle as orc  # noqa: E402
-from gen_golden import BUF_SLICES, OUT, SLICE_PARAMS, checksum, import_reference  # noqa: E402
+from gen_golden import BUF_SLICES, OUT, SLICE_PARAMS, checksum, grad_sample, import_reference  # noqa: E402
 
 LW = 0.1
 LR = 4e-6
@@ -74,6 +74,12 @@ def run_reference_bf16_trunks(ref_model, sd, frames, augmented, spec):
                 wA1=outs[0][2].detach(), wA2=outs[1][2].detach(), grads=grads)
 
 
+def loss_abs_dev(res, r64):
+    """|loss term - fp64| of each of the five terms, in units of the combined fp64 loss (the MSE term is a small
+    difference of two views' maps: its own relative deviation says little)"""
+    return np.abs(res["losses"].double().numpy() - r64["losses"].numpy()) / abs(float(r64["losses"][0]))
+
+
 def deviation(res, r64, names):
     gn = np.array([res["grads"][n].double().norm().item() for n in names])
     g64 = np.array([r64["grads"][n].norm().item() for n in names])
@@ -114,7 +120,15 @@ def make_fixture(ref_model, name, b, t, img_size, freq, frames_t, seed_w=0):
         out["buf_f64/" + n] = r64["bufs"][n][:16].numpy()
     out["nbt_f64"] = np.array([r64["bufs"]["imgnet.bn1.num_batches_tracked"].item(),
                                r64["bufs"]["audnet.bn1.num_batches_tracked"].item()])
-    dev = deviation(run_reference_bf16_trunks(ref_model, sd, frames, augmented, spec), r64, names)
+    for n in names:  # strided samples of every gradient, fp64 and the bf16-autocast yardstick (tests/gradcheck.py)
+        out["grad_sample_f64/" + n] = grad_sample(r64["grads"][n])
+    rb = run_reference_bf16_trunks(ref_model, sd, frames, augmented, spec)
+    for n in names:
+        out["bf16ref_sample/" + n] = grad_sample(rb["grads"][n])
+    for n in SLICE_PARAMS:
+        out["bf16ref_slice/" + n] = rb["grads"][n].flatten()[:64].double().numpy()
+    dev = deviation(rb, r64, names)
+    dev["loss_abs"] = loss_abs_dev(rb, r64)
     for k, v in dev.items():
         out["bf16ref_dev/" + k] = np.asarray(v)
     print(f"[{name}] bf16-trunk reference deviation: " + ", ".join(f"{k}={np.max(v):.3e}" for k, v in dev.items()))
@@ -147,6 +161,8 @@ def main():
     ref_model = import_reference()
     make_fixture(ref_model, "twoview_tiny_b2t3", b=2, t=3, img_size=64, freq=65, frames_t=76)
     make_fixture(ref_model, "twoview_full_b2t2", b=2, t=2, img_size=224, freq=257, frames_t=300)
+    # train_hardway.py's own 16 frames per clip at full size: 32 head rows per view
+    make_fixture(ref_model, "twoview_full_b2t16", b=2, t=16, img_size=224, freq=257, frames_t=300)
 
 
 if __name__ == "__main__":

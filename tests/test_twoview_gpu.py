@@ -18,6 +18,7 @@ from avt_amd.losses import PropagationLoss
 from avt_amd.model import AVENet
 from avt_amd.train import TwoViewTrainStep
 from avt_amd.trunk import P
+from gradcheck import check_grads
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
@@ -193,7 +194,10 @@ def test_flip_loss_module(shape):
 FLOORS = {"logits_off_abs": 2e-2, "logits_diag_rel": 2e-3, "wA_rel": 5e-2}
 
 
-def _check_step(name, g, losses, logits1, wA1, wA2, grad_norms):
+def _check_step(name, g, losses, logits1, wA1, wA2, grads):
+    """logits, weighted_A and the five loss terms against the fp64 reference run, and every parameter gradient
+    against its own bf16-autocast yardstick (tests/gradcheck.check_grads, as the 1-frame tests).  grads: name ->
+    gradient shaped like the Parameter (OIHW)."""
     b, t = g["shape"].tolist()[:2]
     B = b * t
     logits1 = logits1.detach().cpu().double().numpy()
@@ -211,26 +215,22 @@ def _check_step(name, g, losses, logits1, wA1, wA2, grad_norms):
         tol = max(FLOORS[k], 3 * float(g["bf16ref_dev/" + k]))
         print(f"{name}: {k} = {v:.3e} (bf16 reference {float(g['bf16ref_dev/' + k]):.3e}, tol {tol:.3e})")
         assert v <= tol, (k, v, tol)
+    # loss terms: |term - fp64| in units of the combined fp64 loss (the 99.9 x MSE term is a small difference of the
+    # two views' maps, so its own relative error is no measure), each within max(1e-3, 3 x the yardstick's)
     l = losses.detach().cpu().double().numpy()
-    lrel = np.abs(l - g["losses_f64"]) / np.abs(g["losses_f64"])
-    ltol = np.maximum(2e-3, 3 * g["bf16ref_dev/loss_rel"])
-    print(f"{name}: losses {l} ref {g['losses_f64']} rel {lrel} tol {ltol}")
-    assert np.all(lrel <= ltol), (lrel, ltol)
-    names = [str(n) for n in g["param_names"]]
-    gn = np.array([grad_norms[n] for n in names])
-    rel = np.abs(gn - g["grad_norm_f64"]) / g["grad_norm_f64"]
-    dref = g["bf16ref_dev/gradnorm_rel"]
-    # per-parameter bf16 noise is erratic (cancelling BN-weight sums over tiny spatial maps swing by
-    # tens of %); each parameter is bounded by 2x the reference's WORST bf16 deviation, the bulk of the
-    # distribution by 3x its median
-    tol = np.maximum(np.maximum(5e-2, 3 * dref), 2.0 * dref.max())
-    print(f"{name}: grad-norm rel err max {rel.max():.3e} median {np.median(rel):.3e} (bf16 reference max "
-          f"{dref.max():.3e} median {np.median(dref):.3e})")
-    assert np.all(rel <= tol), (names[int((rel / tol).argmax())], rel.max())
-    assert np.median(rel) <= 3 * np.median(dref) + 1e-3
+    labs = np.abs(l - g["losses_f64"]) / abs(float(g["losses_f64"][0]))
+    ltol = np.maximum(1e-3, 3 * g["bf16ref_dev/loss_abs"])
+    print(f"{name}: losses {l} ref {g['losses_f64']} |d|/combined {labs} tol {ltol}")
+    assert np.all(labs <= ltol), (labs, ltol)
+    check_grads(g, grads, tag=name)
 
 
-@pytest.mark.parametrize("name", ["twoview_tiny_b2t3", "twoview_full_b2t2"])
+def _oihw(views):
+    """flat-buffer gradient views (conv weights OHWI) -> the Parameters' OIHW shapes"""
+    return {n: (v.permute(0, 3, 1, 2) if v.dim() == 4 else v) for n, v in views.items()}
+
+
+@pytest.mark.parametrize("name", ["twoview_tiny_b2t3", "twoview_full_b2t2", "twoview_full_b2t16"])
 @pytest.mark.parametrize("dedup", [True, False])
 def test_fused_twoview_step_vs_reference(golden_dir, name, dedup):
     g = _golden(golden_dir, name)
@@ -249,10 +249,9 @@ def test_fused_twoview_step_vs_reference(golden_dir, name, dedup):
     step.engine.forward = spy
     losses = step.step(fr, au, sp)
     torch.cuda.synchronize()
-    views = step.flat.grad_views(step.grad)
-    gnorm = {n: v.norm().item() for n, v in views.items()}
     o1, o2 = outs["views"]
-    _check_step(f"{name}/dedup={dedup}", g, losses, o1["logits"], o1["weighted_A"], o2["weighted_A"], gnorm)
+    _check_step(f"{name}/dedup={dedup}", g, losses, o1["logits"], o1["weighted_A"], o2["weighted_A"],
+                _oihw(step.flat.grad_views(step.grad)))
     sd = model.state_dict()
     from gen_golden import BUF_SLICES
 
@@ -300,8 +299,8 @@ def test_dropin_autograd_twoview_vs_reference(golden_dir):
     combined.backward()
     ref = torch.stack([combined, hardway_loss, aug_loss, l2_loss, consistency]).detach()
     p1 = dict(m1.named_parameters())
-    gnorm = {n: p.grad.norm().item() for n, p in p1.items() if p.grad is not None}
-    _check_step("twoview_tiny_b2t3/drop-in", g, ref, out, weighted, weighted2, gnorm)
+    _check_step("twoview_tiny_b2t3/drop-in", g, ref, out, weighted, weighted2,
+                {n: p.grad for n, p in p1.items() if p.grad is not None})
     assert int(m1.state_dict()["imgnet.bn1.num_batches_tracked"]) == 2
     m2 = _model()
     step = TwoViewTrainStep(m2, lr=lr, weight_decay=wd, loss_weight=lw, dedup_audio=False)

@@ -10,6 +10,9 @@ import avenet_oracle as orc
 from gen_golden import checksum
 
 NAMES = ["twoview_tiny_b2t3", "twoview_full_b2t2"]
+# the 16-frame fixture: its inputs regenerate here; its fp64 oracle run (64 images at 224^2) is left to the generator,
+# which asserts the oracle == the reference on it bit for bit (oracle/gen_golden_twoview.py)
+ALL = NAMES + ["twoview_full_b2t16"]
 
 
 def _load(golden_dir, name):
@@ -21,7 +24,7 @@ def _inputs(g):
     return orc.make_frames(b, t, s, seed=3), orc.make_frames(b, t, s, seed=4), orc.make_spectrogram(b, f, ft)
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", ALL)
 def test_twoview_inputs_regenerate(golden_dir, name):
     g = _load(golden_dir, name)
     fr, au, sp = _inputs(g)
@@ -59,9 +62,10 @@ def test_twoview_oracle_fp64_matches_reference(golden_dir, name):
     assert int(sd["imgnet.bn1.num_batches_tracked"]) == int(g["nbt_f64"][0]) == 2
 
 
-def test_twoview_loss_terms_are_the_reference_formulas(golden_dir):
+@pytest.mark.parametrize("name", ALL)
+def test_twoview_loss_terms_are_the_reference_formulas(golden_dir, name):
     """Loss bookkeeping of train_hardway.py:134-142 on the stored fp64 outputs."""
-    g = _load(golden_dir, "twoview_tiny_b2t3")
+    g = _load(golden_dir, name)
     b, t = g["shape"].tolist()[:2]
     lw = float(g["hyper"][0])
     w1, w2 = torch.from_numpy(g["wA1_f64"]), torch.from_numpy(g["wA2_f64"])
