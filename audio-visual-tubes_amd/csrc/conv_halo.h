@@ -67,8 +67,10 @@ constexpr int halo_blocks_per_cu() {
 // PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop).  Bench-only
 // (tools/halo_bench.hip, profiles/r5_halo_bench_pref.txt): +1..6 % on the layer4 shapes with a 4-stage ring, -3..5 %
 // on layer2; libavt launches PREF = 0
+// OPT (bench-only A/B bits, tools/halo_bench.hip): 1 = waves NW/2 .. NW-1 at s_setprio 1 through the main loop
+// (MI355X_MICROARCH.md "static priority for the younger half")
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
-          int PREF = 0>
+          int PREF = 0, int OPT = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   // fragment geometry: FM x FN MFMA tiles of FR rows per wave, KS k-steps of KD per 64-channel tap
@@ -223,6 +225,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 #pragma unroll
   for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
 
+  if constexpr ((OPT & 1) != 0) {
+    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   bf16x8 af[2][FM], bfr[2][FN];
   auto mma = [&](int buf) {
     if (HALO_DBG(8)) return;
@@ -376,6 +381,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     }
   }
   wait_vmcnt<0>();
+  if constexpr ((OPT & 1) != 0) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
 
   if constexpr (SPLIT) {

@@ -47,9 +47,9 @@ struct Shape {
 
 typedef void (*Launcher)(const GemmNTParams&, const HaloArgs&, int, hipStream_t);
 
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF>
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF, int OPT = 0>
 void launch_v(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false, PREF>), dim3(grid),
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, false, PREF, OPT>), dim3(grid),
                      dim3(WM * WN * 64), 0, st, p, ha);
 }
 
@@ -79,10 +79,11 @@ struct Variant {
   int pk;          // stream-K: needs >= nc units per block
 };
 
-template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF>
+template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF, int OPT = 0>
 Variant make(const char* name) {
   return Variant{name,
-                 {launch_v<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PREF>, launch_v<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PREF>},
+                 {launch_v<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PREF, OPT>,
+                  launch_v<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PREF, OPT>},
                  WM * TM * 32, WN * TN * 32, PRMAX, 0};
 }
 template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PK, int DBG = 0>
@@ -106,9 +107,7 @@ int main(int argc, char** argv) {
   if (argc > 4 && !strcmp(argv[4], "sweep"))  // one / two rounds of 256 tiles (16 x 16 images), K = 18 / 36 / 72 steps
     shapes = {{"s128x1", 256, 16, 16, 128, 128}, {"s256x1", 256, 16, 16, 256, 128}, {"s512x1", 256, 16, 16, 512, 128},
               {"s128x2", 512, 16, 16, 128, 128}, {"s256x2", 512, 16, 16, 256, 128}, {"s512x2", 512, 16, 16, 512, 128}};
-  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make_pk<4, 2, 2, 2, 3, 336, 1>("pk1"),
-                               make_pk<4, 2, 2, 2, 3, 336, 2>("pk2"), make_pk<4, 2, 2, 2, 3, 336, 1, 1>("pk1ns"),
-                               make_pk<4, 2, 2, 2, 3, 336, 1, 3>("pk1nss")};
+  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make<4, 2, 2, 2, 3, 336, 0, 1>("prio")};
   hipStream_t st;
   HIPCHECK(hipStreamCreate(&st));
   hipEvent_t e0, e1;
