@@ -59,19 +59,20 @@ __device__ __forceinline__ int halo_swz(int row) { return (row >> 1) & 7; }
 // NSTB: weight-ring stages.  PRMAX: patch rows the LDS is sized for (>= BM + 2W + 2).
 // EPI: a dgrad with the BatchNorm-backward store epilogue (conv_epi.h; GemmNTParams::bx set).
 // LDS of the main loop (two patch buffers + the weight ring): two blocks per CU when two fit in 160 KB
-template <int WN, int TN, int NSTB, int PRMAX>
+template <int WN, int TN, int NSTB, int PRMAX, int TPS = 1>
 constexpr int halo_blocks_per_cu() {
-  return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
+  return 2 * (2 * (PRMAX * 128 + 1024) + NSTB * TPS * WN * TN * 32 * 128 + 4096) <= 160 * 1024 ? 2 : 1;
 }
 
 // PREF (1, 2): fragments are read PREF k-steps ahead, across the per-step barrier (see the main loop).  Bench-only
 // (tools/halo_bench.hip, profiles/r5_halo_bench_pref.txt): +1..6 % on the layer4 shapes with a 4-stage ring, -3..5 %
 // on layer2; libavt launches PREF = 0
-// OPT (bench-only A/B bits, tools/halo_bench.hip): 1 = waves NW/2 .. NW-1 at s_setprio 1 through the main loop
-// (MI355X_MICROARCH.md "static priority for the younger half")
+// OPT (A/B bits, tools/halo_bench.hip): 1 = waves NW/2 .. NW-1 at s_setprio 1 through the main loop
+// (MI355X_MICROARCH.md "static priority for the younger half"); 2 = two taps per step: one counted wait + block
+// barrier per two taps instead of per tap, NSTB = 2 ring stages of two weight tiles each (see the main loop)
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
           int PREF = 0, int OPT = 0>
-__global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX>())) void conv_halo_kernel(
+__global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX, (OPT & 2) ? 2 : 1>())) void conv_halo_kernel(
     GemmNTParams p, HaloArgs ha) {
   // fragment geometry: FM x FN MFMA tiles of FR rows per wave, KS k-steps of KD per 64-channel tap
   constexpr int FR = 32, FM = TM, FN = TN;
@@ -87,9 +88,10 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   constexpr int AP = (PINSTR + NPIECE * NW - 1) / (NPIECE * NW);  // patch instructions per wave per piece
   constexpr int ABUF = PRMAX * RB + 1024;  // a patch buffer + 8 zero rows (masked taps read them)
   constexpr int BSTAGE = BN * RB;
+  constexpr int TPS = (OPT & 2) ? 2 : 1;  // taps (weight tiles) per ring stage
   constexpr int CT_LD = BN + 8;
   constexpr int EPI_BYTES = BM * CT_LD * 2;
-  constexpr int MAIN = 2 * ABUF + NSTB * BSTAGE;
+  constexpr int MAIN = 2 * ABUF + NSTB * TPS * BSTAGE;
   constexpr int SMEM = (MAIN > EPI_BYTES ? MAIN : EPI_BYTES);
   static_assert(PRMAX % RPI == 0, "PRMAX");
   static_assert(SMEM + 2 * WM * BN * 4 <= 160 * 1024, "LDS budget of a CU");
@@ -220,10 +222,12 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
 #pragma unroll
       for (int v = 0; v < AV; ++v) acc[i][j][v] = 0.f;
 
-  // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2
+  // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2 (two taps per step: step 0's two weight tiles)
   for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, cbase));
+  if constexpr (TPS == 1) {
 #pragma unroll
-  for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
+    for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
+  }
 
   if constexpr ((OPT & 1) != 0) {
     if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -238,7 +242,82 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[buf][i], bfr[buf][j], acc[i][j], 0, 0, 0);
       }
   };
-  if constexpr (PREF) {
+  if constexpr (TPS == 2) {
+    // Two taps per step.  A chunk pair (c, c+1; nchunk is even) is 18 taps = 9 steps; step j of a pair multiplies
+    // pair taps 2j and 2j+1 (pair tap T is tap T % 9 of chunk c + T / 9, whose patch sits in buffer T / 9).  Ring:
+    // 2 stages of two weight tiles; after barrier j a step issues step j+1's two tiles into the stage step j-1 read,
+    // and one quarter of a patch: steps 0-3 chunk c+1's (buffer 1: its last reader, the previous pair's step 8, is
+    // behind barrier 0), steps 5-8 chunk c+2's (buffer 0: last read at step 4).  A step's own patch piece may stay in
+    // flight past the next step's wait, except where the next step reads that patch (steps 4 and 0).  The weight
+    // tiles get one step (two taps) of latency cover, as the one-tap 3-stage ring gives them; the barriers halve.
+    // Accumulation order: the same as the one-tap loop (bitwise equal results).
+    static_assert(NSTB == 2 && !PREF && !SPLIT, "two taps per step: a 2-stage ring, no PREF / split-K");
+    constexpr int AP2 = (PINSTR + 4 * NW - 1) / (4 * NW);  // patch instructions per wave per quarter
+    auto issue_w = [&](int cn, int tn, char* Bs) {
+      const bool live = cn < nchunk;
+      const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + (cbase + cn) * BK) * 2);
+#pragma unroll
+      for (int i = 0; i < BR; ++i)
+        buf_lds16(rsb, Bs + (wid * BR + i) * 1024, (live && !HALO_DBG(1)) ? b_off[i] + boff : kOOB);
+    };
+    auto issue_piece = [&](int cn, int piece) {  // quarter `piece` of chunk cn's patch into buffer cn & 1
+      char* Ab = smem + (cn & 1) * ABUF;
+      const bool alive = cn < nchunk;
+#pragma unroll
+      for (int a = 0; a < AP2; ++a) {
+        const int q = (piece * AP2 + a) * NW + wid;
+        const bool inrange = q < PINSTR;
+        buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow,
+                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase + cn) : kOOB);
+      }
+    };
+    char* const Bring = smem + 2 * ABUF;
+    issue_w(0, 0, Bring);
+    issue_w(0, 1, Bring + BSTAGE);
+    for (int c = 0; c < nchunk; c += 2) {
+      const int sp = (c >> 1) & 1;  // ring stage of this pair's step 0 (9 steps per pair)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        if (j == 0 || j == 4 || j == 5)
+          wait_vmcnt<0>();
+        else
+          wait_vmcnt<AP2>();
+        if (!HALO_DBG(4)) ring_barrier();
+        const int stage = (sp + j) & 1;
+        const char* Bs = Bring + stage * 2 * BSTAGE;
+        auto load_frags = [&](int kk, int buf) {  // k-step kk of this step: tap 2j + kk / KS, k-step kk % KS
+          const int T = 2 * j + kk / KS, ks = kk % KS;
+          const char* Ab = smem + (T / 9) * ABUF;
+          const char* Bt = Bs + (kk / KS) * BSTAGE;
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            af[buf][i] = *reinterpret_cast<const bf16x8*>(Ab + (arow[T % 9][i] ^ (unsigned)(ks << 5)));
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj) bfr[buf][jj] = *reinterpret_cast<const bf16x8*>(Bt + boffs[jj][ks]);
+        };
+        load_frags(0, 0);
+        {
+          char* Bn = Bring + (stage ^ 1) * 2 * BSTAGE;
+          const int T0 = 2 * (j + 1), T1 = T0 + 1;
+          issue_w(c + T0 / 9, T0 % 9, Bn);
+          issue_w(c + T1 / 9, T1 % 9, Bn + BSTAGE);
+          if (j < 4)
+            issue_piece(c + 1, j);
+          else if (j >= 5)
+            issue_piece(c + 2, j - 5);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2 * KS; ++kk) {
+          if (kk + 1 < 2 * KS) {
+            load_frags(kk + 1, (kk + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          mma(kk & 1);
+          if (kk + 1 < 2 * KS) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  } else if constexpr (PREF) {
     // PREF: each step's barrier also publishes the NEXT step's weight tile (and, at a chunk's last tap, the whole
     // next patch), so the next step's first k-step fragments are read during this step's last MFMAs and the
     // MFMAs of a step start right at its barrier -- no LDS round trip between the barrier and the first MFMA.

@@ -77,6 +77,7 @@ struct Variant {
   Launcher fn[2];  // fwd, dgrad
   int BM, BN, PRMAX;
   int pk;          // stream-K: needs >= nc units per block
+  bool tps2;       // two taps per step: an even number of 64-channel chunks
 };
 
 template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PREF, int OPT = 0>
@@ -84,13 +85,13 @@ Variant make(const char* name) {
   return Variant{name,
                  {launch_v<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PREF, OPT>,
                   launch_v<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PREF, OPT>},
-                 WM * TM * 32, WN * TN * 32, PRMAX, 0};
+                 WM * TM * 32, WN * TN * 32, PRMAX, 0, (OPT & 2) != 0};
 }
 template <int WM, int WN, int TM, int TN, int NSTB, int PRMAX, int PK, int DBG = 0>
 Variant make_pk(const char* name) {
   return Variant{name,
                  {launch_pk<MODE_FWD, WM, WN, TM, TN, NSTB, PRMAX, PK, DBG>, launch_pk<MODE_DGRAD, WM, WN, TM, TN, NSTB, PRMAX, PK, DBG>},
-                 WM * TM * 32, WN * TN * 32, PRMAX, PK};
+                 WM * TM * 32, WN * TN * 32, PRMAX, PK, false};
 }
 
 int main(int argc, char** argv) {
@@ -107,7 +108,8 @@ int main(int argc, char** argv) {
   if (argc > 4 && !strcmp(argv[4], "sweep"))  // one / two rounds of 256 tiles (16 x 16 images), K = 18 / 36 / 72 steps
     shapes = {{"s128x1", 256, 16, 16, 128, 128}, {"s256x1", 256, 16, 16, 256, 128}, {"s512x1", 256, 16, 16, 512, 128},
               {"s128x2", 512, 16, 16, 128, 128}, {"s256x2", 512, 16, 16, 256, 128}, {"s512x2", 512, 16, 16, 512, 128}};
-  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make<4, 2, 2, 2, 3, 336, 0, 1>("prio")};
+  std::vector<Variant> vars = {make<4, 2, 2, 2, 3, 336, 0>("base"), make<4, 2, 2, 2, 3, 336, 0, 1>("prio"),
+                               make<4, 2, 2, 2, 2, 336, 0, 2>("tps2"), make<4, 2, 2, 2, 2, 336, 0, 3>("tps2p")};
   hipStream_t st;
   HIPCHECK(hipStreamCreate(&st));
   hipEvent_t e0, e1;
@@ -154,6 +156,7 @@ int main(int argc, char** argv) {
         }
       auto fits = [&](const Variant& V) {
         if (Ng % V.BN != 0 || V.BM + 2 * s.W + 2 > V.PRMAX) return false;
+        if (V.tps2 && (IC / 64) % 2 != 0) return false;  // two taps per step: chunk pairs
         const long long tiles = (M + V.BM - 1) / V.BM * (Ng / V.BN);
         return V.pk != 2 || tiles >= 256;  // stream-K: >= nc units per block
       };
