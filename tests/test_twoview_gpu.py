@@ -265,8 +265,13 @@ def test_fused_twoview_step_vs_reference(golden_dir, name, dedup):
         got = (sd[n].cpu().double() - before[n].double()).flatten()[:64].numpy()
         ref = g["delta_slice_f64/" + n]
         agree = np.mean(np.sign(got) == np.sign(ref))
-        print(f"{n}: sign agreement of first Adam update {agree:.3f}")
-        assert agree > 0.75, n
+        # the first Adam update is ~ -lr sign(g + wd w): a bf16 gradient flips the sign of its near-zero entries.
+        # Bound: 0.75, or the bf16-autocast reference's own agreement on these 64 values less 2 binomial sigmas
+        w0 = before[n].double().flatten()[:64].numpy()
+        a_ref = np.mean(np.sign(-(g["bf16ref_slice/" + n] + wd * w0)) == np.sign(ref))
+        bound = min(0.75, a_ref - 2 * np.sqrt(a_ref * (1 - a_ref) / 64))
+        print(f"{n}: sign agreement of first Adam update {agree:.3f} (bf16 reference {a_ref:.3f}, bound {bound:.3f})")
+        assert agree >= bound, n
         assert np.abs(got).max() <= lr + 1.2e-7, n
 
 
