@@ -22,7 +22,7 @@ def check_grads(g, grads, tag=""):
     256-value strided sample s of each tensor (all of it when smaller; the first 64 values of the
     SLICE_PARAMS as a second sample):
       * error vector   e = |s - s64| / |s64|  <=  max(5e-2, 3 e_ref);
-      * direction      cos(s, s64)  >=  min(0.999, 1 - 3 (1 - cos_ref));
+      * direction      cos(s, s64)  >=  min(0.999, 1 - 3 (1 - cos_ref))  (the strided sample only);
       * norm           | |g| / |g64| - 1 |  <=  max(5e-2, 3 dref, e_ref) -- dref the yardstick's own norm
         deviation, and e_ref its error-vector size: by the triangle inequality a gradient that far from
         the truth may differ in norm by that much.  This matters for the channel-sum gradients (BN
@@ -55,13 +55,16 @@ def check_grads(g, grads, tag=""):
         e, er, c, cr = err(v, ref), err(vb, ref), _cos(v, ref), _cos(vb, ref)
         if kind == "sample":
             e_ref_of[n] = er
-        if c < worst_c[1]:
+        if kind == "sample" and c < worst_c[1]:
             worst_c = (f"{n} ({kind}, yardstick {cr:.4f})", c)
         if e / max(5e-2, 3 * er) > worst_e[1]:
             worst_e = (f"{n} ({kind}: {e:.4f} vs yardstick {er:.4f})", e / max(5e-2, 3 * er))
         if e > max(5e-2, 3 * er):
             bad.append((n, kind, "error", round(e, 4), round(er, 4)))
-        if c < min(0.999, 1 - 3 * (1 - cr)):
+        # direction: on the 256-value strided sample.  A 64-value slice is one filter's contiguous values, whose
+        # bf16 noise is as large as the values (the yardstick's own slice error is 0.4-1.1 at every fixture size):
+        # its cosine swings too far for a 3x rule, so a slice keeps the error-vector bound only
+        if kind == "sample" and c < min(0.999, 1 - 3 * (1 - cr)):
             bad.append((n, kind, "cosine", round(c, 5), round(cr, 5)))
     tol = np.array([max(5e-2, 3 * d, e_ref_of.get(n, 0.0)) for n, d in zip(names, dref)])
     for i, n in enumerate(names):
