@@ -830,13 +830,14 @@ static bool use_small_tile(const GemmNTParams& p, int BN) {
   return blocks128 < (long long)g_small_tile_waves * num_cus();
 }
 
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI>
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI, int OPT = 0>
 static void launch_halo_one(const GemmNTParams& p, const HaloArgs& ha, int grid, hipStream_t st) {
-  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI>), dim3(grid), dim3(WM * WN * 64), 0, st,
-                     p, ha);
+  hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, EPI, false, 0, OPT>), dim3(grid),
+                     dim3(WM * WN * 64), 0, st, p, ha);
 }
 
-template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR>
+// OPT 4: the Conv3d 3x3x3 / stride 1 / pad 1 form (conv_halo.h; forward only)
+template <int MODE, int WM, int WN, int TM, int TN, int NSTB = 3, int PRMAX = kHaloPR, int OPT = 0>
 static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, float* part = nullptr,
                         int* cnt = nullptr) {
   constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -863,6 +864,11 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
       ha.tap_disp[t] = dy * p.OW + dx;
       ha.tap_w[t] = t;
     }
+  if constexpr ((OPT & 4) != 0) {
+    ha.T = p.IT;
+    ha.div_hw = make_magic((unsigned)(p.OH * p.OW));
+    ha.div_t = make_magic((unsigned)p.IT);
+  }
   const int grid = ((p.M + BM - 1) / BM) * (p.Ng / BN) * ksplit;
   if (grid > 0 && ksplit > 1) {
     hipLaunchKernelGGL((conv_halo_kernel<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, true>), dim3(grid),
@@ -870,10 +876,31 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
     return;
   }
   if (grid <= 0) return;
-  if (MODE == MODE_DGRAD && p.bx != nullptr)
+  if constexpr ((OPT & 4) != 0)
+    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, OPT>(p, ha, grid, st);
+  else if (MODE == MODE_DGRAD && p.bx != nullptr)
     launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>(p, ha, grid, st);
   else
     launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false>(p, ha, grid, st);
+}
+
+// Conv3d 3x3x3 / stride 1 / pad 1 with T' = T (the R3D-18 layer2-4 convs, N % 128 == 0, W <= 79) on the halo kernel's
+// three-patch form: avt_set_halo3d / env AVT_HALO3D (1 default, 0 = the tap-gather kernel)
+static int g_halo3d = -1;
+static int halo3d_enabled() {
+  if (g_halo3d < 0) g_halo3d = getenv("AVT_HALO3D") ? atoi(getenv("AVT_HALO3D")) : 1;
+  return g_halo3d;
+}
+static bool halo3d_launch(const GemmNTParams& p, hipStream_t st) {
+  if (!halo3d_enabled() || p.KT != 3 || p.R != 3 || p.S != 3 || p.stride != 1 || p.pad != 1 || p.pad_t != 1 ||
+      p.IT != p.OT || p.IH != p.OH || p.IW != p.OW || p.IC % 64 != 0 || p.Ng % 128 != 0 || conv_variant() != 1 ||
+      256 + 2 * p.OW + 2 > kHaloPR)
+    return false;
+  if (256 + 2 * p.OW + 2 <= 336)
+    launch_halo<MODE_FWD, 4, 2, 2, 2, 3, 336, 4>(p, st);  // 256 x 128, 8 waves, W <= 39
+  else
+    launch_halo<MODE_FWD, 4, 2, 2, 2, 2, kHaloPR, 4>(p, st);  // W <= 79: 2 weight stages to fit the 416-row patches
+  return true;
 }
 
 // the 4-wave 128 x 128 halo tile by weight-ring depth (avt_set_halo_stages / AVT_HALO_NST): 2 stages (80 KB
@@ -1326,6 +1353,7 @@ extern "C" int avt_conv3d_fwd(const void* x, const void* wpack, void* y, double*
               "conv3d_fwd: activation tensors must stay below 2 GiB (32-bit buffer offsets)");
   AVT_REQUIRE(conv_variant() == 1, "conv3d_fwd: needs the LDS-DMA conv kernels (AVT_CONV_VARIANT=1)");
   hipStream_t st = (hipStream_t)stream;
+  if (halo3d_launch(p, st)) return check_launch("conv3d_fwd");
   if (K % 128 == 0)
     launch_nt<MODE_FWD, 8, 128, 128>(p, st);
   else
@@ -1648,6 +1676,12 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
     hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx64, 1), dim3(64), 0, st, slab, pl.groups > 1 ? pl.groups : a.splits,
                        pl.groups > 1 ? pl.per_group : 1, pl.groups > 1 ? pl.groups : a.splits, n, dw);
   }
+}
+
+extern "C" int avt_set_halo3d(int on) {
+  AVT_REQUIRE(on >= -1 && on <= 1, "avt_set_halo3d: %d (0 tap gather, 1 halo, -1 env AVT_HALO3D)", on);
+  g_halo3d = on;
+  return AVT_OK;
 }
 
 extern "C" int avt_set_wgrad_row3(int kg, int min_kt, int pf) {

@@ -31,6 +31,9 @@ struct HaloArgs {
   int* cnt;              // [tiles], zero between launches
   int dbg;               // -DAVT_DIAG build only (AVT_HALO_DBG; wrong results): 1 weight DMA out of range (issued,
                          // no traffic), 2 patch DMA likewise, 4 no per-tap barrier, 8 no MFMA, 16 no epilogue stores
+  // Conv3d 3x3x3 / stride 1 / pad 1 (OPT bit 4): T frames per clip; frame f = (pixel / (H W)) % T
+  int T;
+  MagicDiv div_hw, div_t;
 };
 #ifdef AVT_DIAG
 #define HALO_DBG(bit) (ha.dbg & (bit))
@@ -69,7 +72,13 @@ constexpr int halo_blocks_per_cu() {
 // on layer2; libavt launches PREF = 0
 // OPT (A/B bits, tools/halo_bench.hip): 1 = waves NW/2 .. NW-1 at s_setprio 1 through the main loop
 // (MI355X_MICROARCH.md "static priority for the younger half"); 2 = two taps per step: one counted wait + block
-// barrier per two taps instead of per tap, NSTB = 2 ring stages of two weight tiles each (see the main loop)
+// barrier per two taps instead of per tap, NSTB = 2 ring stages of two weight tiles each (see the main loop);
+// 4 = Conv3d 3x3x3 / stride 1 / pad 1 (fwd): every 64-channel chunk is three "virtual chunks", one per temporal
+// tap dt = -1, 0, 1, each with its own patch -- the input rows [m0 - W - 1 + dt H W, ...) -- read by its 9 spatial
+// taps (weight taps 9 (dt + 1) .. 9 (dt + 1) + 8).  Since the output and input grids coincide (T' = T), an output row
+// in frame f reads frame f + dt of its own clip wherever the spatial tap is valid, except across the clip ends: a
+// patch row is zeroed at the DMA (kOOB) when dt = +1 and its pixel is a clip's frame 0, or dt = -1 and frame T - 1 --
+// rows only an output frame -1 or T would read.  The per-lane spatial tap masks are the 2-D ones.
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI = false, bool SPLIT = false,
           int PREF = 0, int OPT = 0>
 __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRMAX, (OPT & 2) ? 2 : 1>())) void conv_halo_kernel(
@@ -112,7 +121,9 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   const int W = ha.W, H = ha.H, hw = W * H;
   const int pre = W + 1;  // patch row of output pixel m0 is pre
   const int PR = BM + 2 * pre;
-  const int nchunk = SPLIT ? ha.cps : p.IC / BK;  // chunks of this block's K range
+  constexpr int VT = (OPT & 4) ? 3 : 1;  // virtual chunks (temporal taps) per 64-channel chunk
+  static_assert(VT == 1 || (MODE == MODE_FWD && !SPLIT && !EPI), "Conv3d halo: forward, no split-K");
+  const int nchunk = (SPLIT ? ha.cps : p.IC / BK) * VT;  // (virtual) chunks of this block's K range
   const int cbase = SPLIT ? split * ha.cps : 0;
   const int S = nchunk * 9;
 
@@ -126,12 +137,28 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   const int lrow = lane >> 3, pchunk = lane & 7;
   // patch instruction q (of PINSTR) covers patch rows 8q..8q+7; row pr = 8q + lrow holds input pixel
   // m0 - pre + pr, its chunk (pchunk ^ swz) stored at lane position pchunk (source-side swizzle)
-  auto patch_voff = [&](int q, int chunk_c) -> unsigned {
+  // vc: (virtual) chunk index, cbase included
+  auto patch_voff = [&](int q, int vc) -> unsigned {
+    const int chunk_c = vc / VT;
+    const int dt = vc - chunk_c * VT - (VT == 3 ? 1 : 0);
     const int pr = q * RPI + lrow;
-    const int pix = m0 - pre + pr;
+    const int pix = m0 - pre + pr + dt * hw;
     if (q >= PINSTR || pr >= PR || pix < 0 || pix >= p.M) return kOOB;
+    if constexpr (VT == 3) {
+      if (dt != 0) {  // across a clip end (see above)
+        const unsigned f = magic_div((unsigned)pix, ha.div_hw);
+        const unsigned fr = f - magic_div(f, ha.div_t) * (unsigned)ha.T;
+        if (fr == (dt > 0 ? 0u : (unsigned)(ha.T - 1))) return kOOB;
+      }
+    }
     const int lc = pchunk ^ halo_swz(pr);
     return (unsigned)(((long long)pix * p.IC + chunk_c * BK + lc * 8) * 2);
+  };
+  // weight-tile offset of (virtual) chunk vc (cbase included), spatial tap tn: the Conv3d weight operand is
+  // [K][kt][r][s][C], kt = dt + 1
+  auto w_off = [&](int vc, int tn) -> unsigned {
+    const int chunk_c = vc / VT, kt = vc - chunk_c * VT;
+    return (unsigned)(((kt * 9 + ha.tap_w[tn]) * p.IC + chunk_c * BK) * 2);
   };
   unsigned b_off[BR];
 #pragma unroll
@@ -191,7 +218,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
   auto issue = [&](int cn, int tn, int stage) {
     char* Bs = smem + 2 * ABUF + stage * BSTAGE;
     const bool live = cn < nchunk;
-    const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + (cbase + cn) * BK) * 2);
+    const unsigned boff = w_off(cbase * VT + cn, tn);
 #pragma unroll
     for (int i = 0; i < BR; ++i)
       buf_lds16(rsb, Bs + (wid * BR + i) * 1024, (live && !HALO_DBG(1)) ? b_off[i] + boff : kOOB);
@@ -204,7 +231,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const bool inrange = q < PINSTR;
         // out-of-range instructions still issue (constant vmcnt): zeros into the zero area
         buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow,
-                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase + cn + 1) : kOOB);
+                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase * VT + cn + 1) : kOOB);
       }
     }
   };
@@ -223,7 +250,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
       for (int v = 0; v < AV; ++v) acc[i][j][v] = 0.f;
 
   // prologue: chunk 0's whole patch, then steps 0 .. NSTB-2 (two taps per step: step 0's two weight tiles)
-  for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, cbase));
+  for (int q = wid; q < PINSTR; q += NW) buf_lds16(rsa, smem + q * 1024, patch_voff(q, cbase * VT));
   if constexpr (TPS == 1) {
 #pragma unroll
     for (int j = 0; j < NSTB - 1; ++j) issue(0, j, j);
@@ -255,7 +282,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
     constexpr int AP2 = (PINSTR + 4 * NW - 1) / (4 * NW);  // patch instructions per wave per quarter
     auto issue_w = [&](int cn, int tn, char* Bs) {
       const bool live = cn < nchunk;
-      const unsigned boff = (unsigned)((ha.tap_w[tn] * p.IC + (cbase + cn) * BK) * 2);
+      const unsigned boff = w_off(cbase * VT + cn, tn);
 #pragma unroll
       for (int i = 0; i < BR; ++i)
         buf_lds16(rsb, Bs + (wid * BR + i) * 1024, (live && !HALO_DBG(1)) ? b_off[i] + boff : kOOB);
@@ -268,7 +295,7 @@ __global__ __launch_bounds__(WM * WN * 64, (halo_blocks_per_cu<WN, TN, NSTB, PRM
         const int q = (piece * AP2 + a) * NW + wid;
         const bool inrange = q < PINSTR;
         buf_lds16(rsa, inrange ? Ab + q * 1024 : zrow,
-                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase + cn) : kOOB);
+                  (alive && inrange && !HALO_DBG(2)) ? patch_voff(q, cbase * VT + cn) : kOOB);
       }
     };
     char* const Bring = smem + 2 * ABUF;

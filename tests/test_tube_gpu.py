@@ -55,12 +55,25 @@ CONV3D_CASES = [
     (2, 3, 5, 4, 256, 256, 1),
     (1, 16, 14, 14, 256, 512, 2),
     (1, 2, 3, 3, 512, 512, 1),
+    # stride 1, N % 128 == 0: the halo kernel's three-patch Conv3d form (halo3d=1) -- clip ends inside a tile
+    # (several clips, T = 1..16), image widths on both patch-size paths (W <= 39: 336 rows; W = 56: 416), ragged M
+    (2, 4, 9, 11, 128, 128, 1),
+    (3, 1, 14, 14, 128, 256, 1),
+    (3, 5, 28, 28, 128, 128, 1),
+    (1, 3, 56, 56, 128, 128, 1),
+    (2, 16, 14, 14, 512, 512, 1),
+    (1, 7, 13, 17, 256, 128, 1),
 ]
 
 
+@pytest.mark.parametrize("halo3d", [1, 0])
 @pytest.mark.parametrize("case", CONV3D_CASES)
-def test_conv3d_fwd_and_bn_stats(case):
+def test_conv3d_fwd_and_bn_stats(case, halo3d):
+    """Conv3d fwd + its BN statistics vs fp64 torch, on the halo kernel's Conv3d form where it applies (halo3d=1, the
+    default) and on the tap-gather kernel (halo3d=0)."""
     N, T, H, W, C, K, st = case
+    if halo3d == 0 and not (st == 1 and K % 128 == 0):
+        pytest.skip("the halo form does not apply to this shape: halo3d=1 already runs the tap gather")
     g = torch.Generator().manual_seed(11)
     x = torch.randn(N, T, H, W, C, generator=g).relu().to(torch.bfloat16)
     w = (torch.randn(K, C, 3, 3, 3, generator=g) * (2.0 / (K * 27)) ** 0.5).float()
@@ -72,7 +85,11 @@ def test_conv3d_fwd_and_bn_stats(case):
     acc = torch.full((int(query("avt_bn_acc_doubles", N * T * Ho * Wo, K)),), float("nan"), device=DEV,
                      dtype=torch.float64)
     xd = x.to(DEV)
-    call("avt_conv3d_fwd", P(xd), P(wp), P(y), P(acc), N, T, H, W, C, K, 3, 3, 3, st, 1, 1, S())
+    try:
+        call("avt_set_halo3d", halo3d)
+        call("avt_conv3d_fwd", P(xd), P(wp), P(y), P(acc), N, T, H, W, C, K, 3, 3, 3, st, 1, 1, S())
+    finally:
+        call("avt_set_halo3d", -1)
     ref = F.conv3d(x.double().permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).double(), stride=(1, st, st), padding=1)
     ref = ref.permute(0, 2, 3, 4, 1)
     err = rel_err(y, ref)
@@ -108,6 +125,7 @@ def test_conv3d_tile_configs(C, K):
             [("avt_set_nt128_config", v) for v in (-1, 1, 6)]
     outs = []
     try:
+        call("avt_set_halo3d", 0)  # the tap-gather tiles (the halo form takes K % 128 == 0 by default)
         for fn, v in knobs:
             call(fn, v)
             y = torch.empty(N, T, H, W, K, device=DEV, dtype=torch.bfloat16)
@@ -117,6 +135,7 @@ def test_conv3d_tile_configs(C, K):
     finally:
         call("avt_set_nt64_config", -1)
         call("avt_set_nt128_config", -1)
+        call("avt_set_halo3d", -1)
     for (fn, v), o in zip(knobs[1:], outs[1:]):
         assert torch.equal(o, outs[0]), (fn, v)
     # output frames 0 and 1 read input frames 0-2 only

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--nt64", default="-1")
     ap.add_argument("--nt128", default="-1")
+    ap.add_argument("--halo3d", default="1,0", help="avt_set_halo3d values to sweep (1: the halo Conv3d form where it "
+                    "applies, 0: the tap-gather kernel)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     b, T = args.clips, args.frames
@@ -50,14 +52,19 @@ def main():
         line = f"{name:10s} M={b * T * Ho * Wo:8d} N={K:4d} K={27 * C:5d} |"
         cfgs = [("nt64", int(v)) for v in args.nt64.split(",")] if K == 64 else \
                [("nt128", int(v)) for v in args.nt128.split(",")]
+        if K % 128 == 0 and st == 1:
+            cfgs = [("halo3d", int(v)) for v in args.halo3d.split(",")] + [c for c in cfgs if c != ("nt128", -1)]
         for knob, v in cfgs:
-            call("avt_set_nt64_config" if knob == "nt64" else "avt_set_nt128_config", v)
+            call("avt_set_halo3d", v if knob == "halo3d" else 0)
+            if knob != "halo3d":
+                call("avt_set_nt64_config" if knob == "nt64" else "avt_set_nt128_config", v)
             ms = timeit(lambda: call("avt_conv3d_fwd", P(x), P(wf), P(y), None, b, T, H, W, C, K, 3, 3, 3, st, 1, 1,
                                      S()))
             line += f" {knob}[{v}] {flops / ms / 1e9:5.0f} ({ms * 1e3:6.1f} us)"
             total[(knob, v)] = total.get((knob, v), 0.0) + ms
         call("avt_set_nt64_config", -1)
         call("avt_set_nt128_config", -1)
+        call("avt_set_halo3d", -1)
         print(line, flush=True)
     print({f"{k}[{v}]": round(ms, 3) for (k, v), ms in total.items()}, "ms total")
 

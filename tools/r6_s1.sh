@@ -4,7 +4,9 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
 step() { local name=$1; shift; "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 "gpurun_out/$name.log"; exit $rc; }; }
-step t_new timeout -k 10 480 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_bench_dist_gpu.py \
+# a test failure (rc 1) is not a GPU fault: record it and go on; anything else (timeout, abort, segfault) stops
+soft() { local name=$1; shift; "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || { tail -20 "gpurun_out/$name.log"; exit $rc; }; [ $rc -eq 0 ] || tail -25 "gpurun_out/$name.log"; }
+soft t_new timeout -k 10 480 python -u -m pytest -v --timeout 400 --timeout-method thread tests/test_bench_dist_gpu.py \
   "tests/test_ddp_gpu.py::test_side_stream_adam_ordering_without_host_sync" \
   "tests/test_model_gpu.py::test_eval_mode_input_gradient_refused" tests/test_twoview_gpu.py
 step smoke timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()"
