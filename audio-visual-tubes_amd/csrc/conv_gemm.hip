@@ -879,9 +879,20 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
   if constexpr ((OPT & 4) != 0)
     launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, OPT>(p, ha, grid, st);
   else if (MODE == MODE_DGRAD && p.bx != nullptr)
-    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, true>(p, ha, grid, st);
+    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, true, OPT>(p, ha, grid, st);
   else
-    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false>(p, ha, grid, st);
+    launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, OPT>(p, ha, grid, st);
+}
+
+// the 8-wave 256 x 128 halo tile with two taps per barrier and waves 4-7 at s_setprio 1 (conv_halo.h OPT 3) for the
+// long-K convs (>= 8 (virtual) chunks: the 2-D layer4, C = 512; the Conv3d layer3/4): +3..11 % per shape at B=128 in
+// tools/halo_bench (profiles/r6_halo_bench_prio_tps2.txt), -1..2 % on the 2-4-chunk layer2/3 shapes, which keep the
+// one-tap loop.  avt_set_halo_tps2 / env AVT_HALO_TPS2 (1 default, 0 off; -1 back to the environment)
+static int g_halo_tps2 = -1;
+static int halo_tps2(const GemmNTParams& p, int vt = 1) {
+  if (g_halo_tps2 < 0) g_halo_tps2 = getenv("AVT_HALO_TPS2") ? atoi(getenv("AVT_HALO_TPS2")) : 1;
+  const int nv = p.IC / 64 * vt;
+  return g_halo_tps2 && p.IC % 64 == 0 && nv % 2 == 0 && nv >= 8;
 }
 
 // Conv3d 3x3x3 / stride 1 / pad 1 with T' = T (the R3D-18 layer2-4 convs, N % 128 == 0, W <= 79) on the halo kernel's
@@ -896,7 +907,9 @@ static bool halo3d_launch(const GemmNTParams& p, hipStream_t st) {
       p.IT != p.OT || p.IH != p.OH || p.IW != p.OW || p.IC % 64 != 0 || p.Ng % 128 != 0 || conv_variant() != 1 ||
       256 + 2 * p.OW + 2 > kHaloPR)
     return false;
-  if (256 + 2 * p.OW + 2 <= 336)
+  if (256 + 2 * p.OW + 2 <= 336 && halo_tps2(p, 3))
+    launch_halo<MODE_FWD, 4, 2, 2, 2, 2, 336, 7>(p, st);  // 256 x 128, 8 waves, W <= 39, two taps per barrier
+  else if (256 + 2 * p.OW + 2 <= 336)
     launch_halo<MODE_FWD, 4, 2, 2, 2, 3, 336, 4>(p, st);  // 256 x 128, 8 waves, W <= 39
   else
     launch_halo<MODE_FWD, 4, 2, 2, 2, 2, kHaloPR, 4>(p, st);  // W <= 79: 2 weight stages to fit the 416-row patches
@@ -1063,6 +1076,8 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
           launch_halo<MODE, 2, 2, 4, 2, 3, 336>(p, st);  // same tile on 4 waves of 128 x 64 (0.75 KB LDS per MFMA)
         else if (halo8_nst() == 4)
           launch_halo<MODE, 4, 2, 2, 2, 4, 336>(p, st);  // 4-stage weight ring: 150 KB of LDS, still 1 block/CU
+        else if (halo_tps2(p))
+          launch_halo<MODE, 4, 2, 2, 2, 2, 336, 3>(p, st);  // ... two taps per barrier (layer4)
         else
           launch_halo<MODE, 4, 2, 2, 2, 3, 336>(p, st);  // 256 x 128, 8 waves, W <= 39 (layer2)
       }
@@ -1676,6 +1691,12 @@ static void launch_wgrad_halo(WgradHaloPlan& pl, const bf16_t* x, const bf16_t* 
     hipLaunchKernelGGL(wgrad_halo_reduce_kernel, dim3(gx64, 1), dim3(64), 0, st, slab, pl.groups > 1 ? pl.groups : a.splits,
                        pl.groups > 1 ? pl.per_group : 1, pl.groups > 1 ? pl.groups : a.splits, n, dw);
   }
+}
+
+extern "C" int avt_set_halo_tps2(int on) {
+  AVT_REQUIRE(on >= -1 && on <= 1, "avt_set_halo_tps2: %d (0 one tap per barrier, 1 two, -1 env AVT_HALO_TPS2)", on);
+  g_halo_tps2 = on;
+  return AVT_OK;
 }
 
 extern "C" int avt_set_halo3d(int on) {

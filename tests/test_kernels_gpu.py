@@ -1083,7 +1083,8 @@ def test_small_grid_conv_repeatable(case):
 @pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (2, 33, 38, 128, 128, 3, 1, 1)])
 def test_halo8_form_and_ring_bitwise_equal(case):
     """The 8-wave 256 x 128 halo tile's A/B knobs (avt_set_halo8_form: 4 waves of 128 x 64; avt_set_halo8_nst:
-    a 4-stage weight ring) change the wave layout and the DMA depth, not the k order of any output: conv
+    a 4-stage weight ring; avt_set_halo_tps2: one wait + barrier per two taps, the default for >= 8 chunks) change
+    the wave layout, the DMA depth and the synchronisation, not the k order of any output: conv
     outputs, plain dgrads and BN-epilogue dgrads are bitwise equal; the BN slot sums are bitwise equal under the
     4-stage ring and equal to rounding under the 4-wave form (its reduction partition differs)."""
     N, H, W, C, K, R, st, pad = case
@@ -1098,9 +1099,10 @@ def test_halo8_form_and_ring_bitwise_equal(case):
     call("avt_set_halo8", 1)
     outs = []
     try:
-        for form, nst in ((0, 3), (1, 3), (0, 4)):
+        for form, nst, tps2 in ((0, 3, 0), (1, 3, 0), (0, 4, 0), (0, 3, 1)):
             call("avt_set_halo8_form", form)
             call("avt_set_halo8_nst", nst)
+            call("avt_set_halo_tps2", tps2)
             y = torch.empty(N, H, W, K, device=DEV, dtype=torch.bfloat16)
             acc = fwd_acc(N * H * W, K)
             call("avt_conv2d_fwd", P(x), P(wf), P(y), P(acc), N, H, W, C, K, R, R, st, pad, R * R * C, S())
@@ -1117,10 +1119,11 @@ def test_halo8_form_and_ring_bitwise_equal(case):
     finally:
         call("avt_set_halo8_form", -1)
         call("avt_set_halo8_nst", -1)
+        call("avt_set_halo_tps2", -1)
         call("avt_set_halo8", -1)
     # outputs and dgrads bitwise; the 4-wave form sums the statistics over its own wave/thread partition (another
-    # fp32 order): its slots to rounding, the 4-stage ring's bitwise
-    for form, o in zip((1, 0), outs[1:]):
+    # fp32 order): its slots to rounding, the 4-stage ring's and the two-tap loop's bitwise
+    for form, o in zip((1, 0, 0), outs[1:]):
         for a, b in zip(o[:3], outs[0][:3]):
             assert torch.equal(a, b)
         for a, b in zip(o[3:], outs[0][3:]):

@@ -109,6 +109,34 @@ def test_conv3d_fwd_and_bn_stats(case, halo3d):
                                atol=1e-4 * var.max().item())
 
 
+@pytest.mark.parametrize("case", [(2, 16, 14, 14, 512, 512), (3, 5, 9, 11, 256, 128), (1, 4, 28, 28, 256, 256)])
+def test_conv3d_halo_two_tap_bitwise(case):
+    """The Conv3d halo form with one wait + barrier per two taps (avt_set_halo_tps2(1), the default for >= 8 virtual
+    chunks: the R3D-18 layer3/4) and per tap (0): the same k order, bitwise-equal outputs and BN slots."""
+    N, T, H, W, C, K = case
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, T, H, W, C, generator=g).relu().to(torch.bfloat16).to(DEV)
+    w = (torch.randn(K, C, 3, 3, 3, generator=g) * (2.0 / (K * 27)) ** 0.5).float().to(DEV)
+    wp = torch.empty(K, 27 * C, device=DEV, dtype=torch.bfloat16)
+    call("avt_pack_conv3d_weight", P(w), P(wp), K, C, 3, 3, 3, 0, S())
+    rows = N * T * H * W
+    outs = []
+    try:
+        for tps2 in (0, 1):
+            call("avt_set_halo_tps2", tps2)
+            y = torch.empty(N, T, H, W, K, device=DEV, dtype=torch.bfloat16)
+            acc = torch.full((int(query("avt_bn_acc_doubles", rows, K)),), float("nan"), device=DEV,
+                             dtype=torch.float64)
+            call("avt_conv3d_fwd", P(x), P(wp), P(y), P(acc), N, T, H, W, C, K, 3, 3, 3, 1, 1, 1, S())
+            torch.cuda.synchronize()
+            nslots = (rows + 255) // 256
+            outs.append((y.view(torch.int16).clone(), acc[:8 + nslots * K * 3].clone()))  # header + the written slots
+    finally:
+        call("avt_set_halo_tps2", -1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("C,K", [(64, 64), (64, 128), (128, 128)])
 def test_conv3d_tile_configs(C, K):
     """Conv3d at a GEMM M >= 65536 (where the tile choice depends on K) under every tile config the
