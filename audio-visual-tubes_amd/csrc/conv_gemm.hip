@@ -904,9 +904,14 @@ static int halo3d_enabled() {
 }
 static bool halo3d_launch(const GemmNTParams& p, hipStream_t st) {
   if (!halo3d_enabled() || p.KT != 3 || p.R != 3 || p.S != 3 || p.stride != 1 || p.pad != 1 || p.pad_t != 1 ||
-      p.IT != p.OT || p.IH != p.OH || p.IW != p.OW || p.IC % 64 != 0 || p.Ng % 128 != 0 || conv_variant() != 1 ||
-      256 + 2 * p.OW + 2 > kHaloPR)
+      p.IT != p.OT || p.IH != p.OH || p.IW != p.OW || p.IC % 64 != 0 || conv_variant() != 1)
     return false;
+  if (p.Ng == 64) {  // R3D-18 layer1 (K = 64, W = 112): 256 x 64 on 8 waves of 32 x 64, a 488-row patch (W <= 115)
+    if (halo3d_enabled() < 2 || 256 + 2 * p.OW + 2 > 488) return false;  // A/B (avt_set_halo3d(2))
+    launch_halo<MODE_FWD, 8, 1, 1, 2, 3, 488, 4>(p, st);
+    return true;
+  }
+  if (p.Ng % 128 != 0 || 256 + 2 * p.OW + 2 > kHaloPR) return false;
   if (256 + 2 * p.OW + 2 <= 336 && halo_tps2(p, 3))
     launch_halo<MODE_FWD, 4, 2, 2, 2, 2, 336, 7>(p, st);  // 256 x 128, 8 waves, W <= 39, two taps per barrier
   else if (256 + 2 * p.OW + 2 <= 336)
@@ -1700,7 +1705,8 @@ extern "C" int avt_set_halo_tps2(int on) {
 }
 
 extern "C" int avt_set_halo3d(int on) {
-  AVT_REQUIRE(on >= -1 && on <= 1, "avt_set_halo3d: %d (0 tap gather, 1 halo, -1 env AVT_HALO3D)", on);
+  AVT_REQUIRE(on >= -1 && on <= 2, "avt_set_halo3d: %d (0 tap gather, 1 halo for K %% 128 == 0, 2 also K = 64, -1 env "
+              "AVT_HALO3D)", on);
   g_halo3d = on;
   return AVT_OK;
 }

@@ -52,8 +52,9 @@ def main():
         line = f"{name:10s} M={b * T * Ho * Wo:8d} N={K:4d} K={27 * C:5d} |"
         cfgs = [("nt64", int(v)) for v in args.nt64.split(",")] if K == 64 else \
                [("nt128", int(v)) for v in args.nt128.split(",")]
-        if K % 128 == 0 and st == 1:
-            cfgs = [("halo3d", int(v)) for v in args.halo3d.split(",")] + [c for c in cfgs if c != ("nt128", -1)]
+        if st == 1 and (K % 128 == 0 or K == 64):  # (K = 64: the halo form only under avt_set_halo3d(2))
+            cfgs = [("halo3d", int(v)) for v in args.halo3d.split(",")] + \
+                   [c for c in cfgs if c not in (("nt128", -1), ("nt64", -1))]
         for knob, v in cfgs:
             call("avt_set_halo3d", v if knob == "halo3d" else 0)
             if knob != "halo3d":

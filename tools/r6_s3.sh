@@ -9,7 +9,7 @@ soft t_tube timeout -k 10 400 python -u -m pytest -q --timeout 300 --timeout-met
   "tests/test_kernels_gpu.py::test_halo8_form_and_ring_bitwise_equal"
 step dconv3d timeout -k 10 200 python tools/diag_conv3d.py
 step c3d timeout -k 10 200 env AVT_HALO_TPS2=1 python tools/conv3d_bench.py --halo3d 1,0
-step c3d0 timeout -k 10 200 env AVT_HALO_TPS2=0 python tools/conv3d_bench.py --halo3d 1
+step c3d0 timeout -k 10 200 env AVT_HALO_TPS2=0 python tools/conv3d_bench.py --halo3d 1,2
 export BENCH_ARGS="--traffic off --no-peaks --steps 20 --warmup 5"
 step ab_b128 bash tools/ab3.sh 3 "tps2:AVT_HALO_TPS2=1" "one:AVT_HALO_TPS2=0"
 export BENCH_ARGS="--workload tube --traffic off --no-peaks --steps 10 --warmup 3"
