@@ -884,22 +884,25 @@ static void launch_halo(const GemmNTParams& p, hipStream_t st, int ksplit = 1, f
     launch_halo_one<MODE, WM, WN, TM, TN, NSTB, PRMAX, false, OPT>(p, ha, grid, st);
 }
 
-// the 8-wave 256 x 128 halo tile with two taps per barrier and waves 4-7 at s_setprio 1 (conv_halo.h OPT 3) for the
-// long-K convs (>= 8 (virtual) chunks: the 2-D layer4, C = 512; the Conv3d layer3/4): +3..11 % per shape at B=128 in
-// tools/halo_bench (profiles/r6_halo_bench_prio_tps2.txt), -1..2 % on the 2-4-chunk layer2/3 shapes, which keep the
-// one-tap loop.  avt_set_halo_tps2 / env AVT_HALO_TPS2 (1 default, 0 off; -1 back to the environment)
+// A/B knob: the 8-wave 256 x 128 halo tile with two taps per barrier and waves 4-7 at s_setprio 1 (conv_halo.h OPT 3)
+// for the long-K convs (>= 8 (virtual) chunks: the 2-D layer4, C = 512; the Conv3d layer3/4).  +3..11 % per shape at
+// B=128 in tools/halo_bench on random operands (profiles/r6_halo_bench_prio_tps2.txt), but +-0.1 % on the B=128 step
+// (profiles/r6_ab_tps2_b128.txt) and +-2 % on the Conv3d shapes (r6_conv3d_halo.txt): off by default.
+// avt_set_halo_tps2 / env AVT_HALO_TPS2 (0 default, 1 on; -1 back to the environment)
 static int g_halo_tps2 = -1;
 static int halo_tps2(const GemmNTParams& p, int vt = 1) {
-  if (g_halo_tps2 < 0) g_halo_tps2 = getenv("AVT_HALO_TPS2") ? atoi(getenv("AVT_HALO_TPS2")) : 1;
+  if (g_halo_tps2 < 0) g_halo_tps2 = getenv("AVT_HALO_TPS2") ? atoi(getenv("AVT_HALO_TPS2")) : 0;
   const int nv = p.IC / 64 * vt;
   return g_halo_tps2 && p.IC % 64 == 0 && nv % 2 == 0 && nv >= 8;
 }
 
-// Conv3d 3x3x3 / stride 1 / pad 1 with T' = T (the R3D-18 layer2-4 convs, N % 128 == 0, W <= 79) on the halo kernel's
-// three-patch form: avt_set_halo3d / env AVT_HALO3D (1 default, 0 = the tap-gather kernel)
+// Conv3d 3x3x3 / stride 1 / pad 1 with T' = T on the halo kernel's three-patch form: the R3D-18 layer2-4 convs (N %
+// 128 == 0, W <= 79; 256 x 128 tile) and layer1 (N = 64, W <= 115; 256 x 64 tile).  Per shape at b=8 x 16 frames
+// (profiles/r6_conv3d_halo.txt) 1094-1209 TFLOP/s against 886-928 for the tap gather on layer2-4, 789 against 549-635 on
+// layer1.  avt_set_halo3d / env AVT_HALO3D: 2 (default) both, 1 layer2-4 only, 0 the tap-gather kernel
 static int g_halo3d = -1;
 static int halo3d_enabled() {
-  if (g_halo3d < 0) g_halo3d = getenv("AVT_HALO3D") ? atoi(getenv("AVT_HALO3D")) : 1;
+  if (g_halo3d < 0) g_halo3d = getenv("AVT_HALO3D") ? atoi(getenv("AVT_HALO3D")) : 2;
   return g_halo3d;
 }
 static bool halo3d_launch(const GemmNTParams& p, hipStream_t st) {
@@ -907,7 +910,7 @@ static bool halo3d_launch(const GemmNTParams& p, hipStream_t st) {
       p.IT != p.OT || p.IH != p.OH || p.IW != p.OW || p.IC % 64 != 0 || conv_variant() != 1)
     return false;
   if (p.Ng == 64) {  // R3D-18 layer1 (K = 64, W = 112): 256 x 64 on 8 waves of 32 x 64, a 488-row patch (W <= 115)
-    if (halo3d_enabled() < 2 || 256 + 2 * p.OW + 2 > 488) return false;  // A/B (avt_set_halo3d(2))
+    if (halo3d_enabled() < 2 || 256 + 2 * p.OW + 2 > 488) return false;
     launch_halo<MODE_FWD, 8, 1, 1, 2, 3, 488, 4>(p, st);
     return true;
   }

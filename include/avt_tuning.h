@@ -76,12 +76,13 @@ int avt_set_wgrad_halo(int on);
  * read behind the current tile's MFMAs (1, env AVT_ROW3_PF, default) or after its barrier (0); -1 resets a value
  * to its environment default */
 int avt_set_wgrad_row3(int kg, int min_kt, int pf);
-/* 1 (default, env AVT_HALO3D): the Conv3d 3x3x3 / stride 1 / pad 1 convs with N % 128 == 0 and W <= 79 (R3D-18
- * layer2-4) on the halo kernel's three-patch form; 0: the tap-gather kernel; -1: back to the environment default */
+/* the Conv3d 3x3x3 / stride 1 / pad 1 convs on the halo kernel's three-patch form -- 2 (default, env AVT_HALO3D): the
+ * N % 128 == 0, W <= 79 ones (R3D-18 layer2-4) and the N = 64, W <= 115 ones (layer1); 1: the former only; 0: all on
+ * the tap-gather kernel; -1: back to the environment default */
 int avt_set_halo3d(int on);
-/* 1 (default, env AVT_HALO_TPS2): the 8-wave 256 x 128 halo fwd/dgrad of the >= 8-chunk (C >= 512) convs waits and
- * synchronises once per two taps (a 2-stage ring of two weight tiles) with waves 4-7 at s_setprio 1; 0: once per
- * tap (3-stage ring); -1: back to the environment default.  Bitwise-equal results either way */
+/* A/B knob, 0 by default (env AVT_HALO_TPS2): 1 = the 8-wave 256 x 128 halo fwd/dgrad of the >= 8-chunk convs waits
+ * and synchronises once per two taps (a 2-stage ring of two weight tiles) with waves 4-7 at s_setprio 1; -1: back to
+ * the environment default.  Bitwise-equal results either way */
 int avt_set_halo_tps2(int on);
 /* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
  * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */

@@ -1083,7 +1083,7 @@ def test_small_grid_conv_repeatable(case):
 @pytest.mark.parametrize("case", [(2, 17, 19, 512, 512, 3, 1, 1), (2, 33, 38, 128, 128, 3, 1, 1)])
 def test_halo8_form_and_ring_bitwise_equal(case):
     """The 8-wave 256 x 128 halo tile's A/B knobs (avt_set_halo8_form: 4 waves of 128 x 64; avt_set_halo8_nst:
-    a 4-stage weight ring; avt_set_halo_tps2: one wait + barrier per two taps, the default for >= 8 chunks) change
+    a 4-stage weight ring; avt_set_halo_tps2: one wait + barrier per two taps for >= 8 chunks, an A/B knob) change
     the wave layout, the DMA depth and the synchronisation, not the k order of any output: conv
     outputs, plain dgrads and BN-epilogue dgrads are bitwise equal; the BN slot sums are bitwise equal under the
     4-stage ring and equal to rounding under the 4-wave form (its reduction partition differs)."""
