@@ -668,7 +668,7 @@ static void launch_pipe_one(const GemmNTParams& p, const NTPipeArgsV& ta0, hipSt
     ta.cdiv_hw[k] = make_magic((unsigned)(oh > 0 && ow > 0 ? oh * ow : 1));
     ta.cdiv_ow[k] = make_magic((unsigned)(ow > 0 ? ow : 1));
   }
-  if (p.IT > 1 || p.OT > 1 || ta.ntaps > 32) {  // Conv3d / the folded 49-tap video stem
+  if (p.IT > 1 || p.OT > 1 || p.KT > 1 || ta.ntaps > 32) {  // Conv3d / the folded 49-tap video stem
     if constexpr (MODE == MODE_FWD)
       hipLaunchKernelGGL((conv_nt_pipe_kernel<MODE, WM, WN, TM, TN, NST, BK, true>), dim3(grid), dim3(WM * WN * 64), 0,
                          st, p, ta);
@@ -803,7 +803,7 @@ constexpr int kHaloPR = 416;  // patch rows the halo kernels' LDS holds: 256 + 2
 // 3x3 / stride 1 / pad 1 Conv2d, 64-channel multiples, image width <= 79: the halo-reuse kernel
 static bool halo_eligible(const GemmNTParams& p) {
   const int h = halo_enabled();
-  if (!h || p.R != 3 || p.S != 3 || p.stride != 1 || p.pad != 1 || p.IC % 64 != 0 || p.IT > 1 || p.OT > 1 ||
+  if (!h || p.R != 3 || p.S != 3 || p.stride != 1 || p.pad != 1 || p.IC % 64 != 0 || p.IT > 1 || p.OT > 1 || p.KT > 1 ||
       p.IH != p.OH || p.IW != p.OW)
     return false;
   if (h == 2) return 256 + 2 * p.OW + 2 <= kHaloPR && (p.Ng % 128 == 0 || p.Ng == 64);  // 8-wave forms (A/B)
@@ -984,7 +984,7 @@ static int halo_splitk(const GemmNTParams& p) {
 // tap-gather kernel everywhere, as the bitwise-order tests need) or avt_set_c64(0)
 static bool c64_eligible(const GemmNTParams& p) {
   return c64_enabled() && halo_enabled() && conv_variant() == 1 && p.IC == 64 && p.Ng == 64 && p.Kg == 576 &&
-         p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.IT == 1 && p.OT == 1 && p.IH == p.OH &&
+         p.R == 3 && p.S == 3 && p.stride == 1 && p.pad == 1 && p.IT == 1 && p.OT == 1 && p.KT == 1 && p.IH == p.OH &&
          p.IW == p.OW && 256 + 2 * p.OW + 2 <= c64::PRMAX && p.bx == nullptr && (p.add == nullptr || p.add != p.out);
 }
 
@@ -1046,7 +1046,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     launch_c64<MODE>(p, st);
     return;
   }
-  if (CVEC == 8 && ws != nullptr && p.IT == 1 && p.OT == 1) {
+  if (CVEC == 8 && ws != nullptr && p.IT == 1 && p.OT == 1 && p.KT == 1) {
     const int ks = halo_splitk(p);
     const long long tiles = (long long)((p.M + 127) / 128) * (p.Ng / 128);
     // the plan is re-made at every call from the current knobs: a workspace sized for another plan
@@ -1056,7 +1056,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
       return;
     }
   }
-  if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && g_nt128_config < 0 && (g_nt64_config < 0 || g_nt64_config == 1) &&
+  if (CVEC == 8 && conv_variant() == 1 && p.IT == 1 && p.OT == 1 && p.KT == 1 && g_nt128_config < 0 && (g_nt64_config < 0 || g_nt64_config == 1) &&
       p.bx == nullptr && use_small_tile(p, p.Ng % 128 == 0 ? 128 : 64)) {
     if (p.Ng % 128 == 0) {
       if (halo_eligible(p) && 64 + 2 * p.OW + 2 <= 104) {  // 64 x 128 halo tile
@@ -1105,7 +1105,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
       // Conv3d (27 taps: 3x the K of a 3x3) keeps the 128 x 128 k64 tile unless K is short: on the R3D-18
       // trunk (tools/conv3d_bench.py, profiles/r5_conv3d_tiles.txt) it is 10-15 % faster than the 256-row
       // form on layer2/3's 3x3x3 convs; at layer2.0's K = 1728 the two are within 3 %
-      const bool vid = p.IT > 1 || p.OT > 1;
+      const bool vid = p.IT > 1 || p.OT > 1 || p.KT > 1;
       const int cfg = g_nt128_config >= 0 ? g_nt128_config : (p.M >= 65536 && (!vid || p.Kg < 3072) ? 6 : 1);
       switch (cfg) {
         case 1: launch_glds<MODE, 2, 2, 2, 2, 2, 64>(p, st); break;  // 128 x 128, k64, 2 stages
@@ -1119,7 +1119,7 @@ static void launch_nt(const GemmNTParams& p, hipStream_t st, const SplitWs* ws =
     } else {  // 64-wide N (layer1 / stem-fed convs)
       // auto (-1): 1, or 2 (4 stages) for a Conv3d -- R3D-18 layer1, profiles/r5_conv3d_tiles.txt: 548-579 us
       // against 557-683 us per conv, ahead in every ordering measured
-      switch (g_nt64_config >= 0 ? g_nt64_config : (p.IT > 1 || p.OT > 1 ? 2 : 1)) {
+      switch (g_nt64_config >= 0 ? g_nt64_config : (p.IT > 1 || p.OT > 1 || p.KT > 1 ? 2 : 1)) {
         case 0: launch_glds<MODE, 4, 1, 2, 2, 4>(p, st); break;  // 256 x 64, 4 stages
         case 2: launch_glds<MODE, 2, 2, 2, 1, 4>(p, st); break;  // 128 x 64, 4 stages
         case 3: launch_glds<MODE, 4, 1, 2, 2, 2>(p, st); break;  // 256 x 64, 2 stages
