@@ -762,7 +762,7 @@ extern "C" int avt_bn_apply(const void* x, const float* scale, const float* shif
   AVT_REQUIRE(C % 8 == 0, "bn_apply: C=%d must be a multiple of 8", C);
   AVT_REQUIRE((rscale == nullptr) == (rshift == nullptr), "bn_apply: rscale/rshift must be both set or both null");
   const long long nvec = rows * C / 8;
-  if (nvec == 0) return AVT_OK;
+  if (nvec == 0 || diag_skip(16, (hipStream_t)stream)) return AVT_OK;
   const int grid = ew_grid(nvec);
   if (256 % (C / 8) == 0)
     hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x, scale,
@@ -780,7 +780,7 @@ extern "C" int avt_bn_apply_mask(const void* x, const float* scale, const float*
   AVT_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_apply_mask: C=%d unsupported", C);
   AVT_REQUIRE((rscale == nullptr) == (rshift == nullptr), "bn_apply_mask: rscale/rshift must be both set or both null");
   const long long nvec = rows * C / 8;
-  if (nvec == 0) return AVT_OK;
+  if (nvec == 0 || diag_skip(16, (hipStream_t)stream)) return AVT_OK;
   hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(ew_grid(nvec)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                      scale, shift, (const bf16_t*)residual, rscale, rshift, (bf16_t*)out, (unsigned char*)mask, nvec, C,
                      1);
@@ -838,7 +838,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.nvec = rows * C / 8;
   p.C = C;
   if (t2) {
-    hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
+    if (!diag_skip(8, st)) hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
     if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + kFinCB - 1) / kFinCB)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
@@ -850,7 +850,7 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     p.gc2 = (bf16_t*)t2->gc;
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
-    hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
+    if (!diag_skip(8, st)) hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
     if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
@@ -875,8 +875,9 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
-                       rows, C, st);
+  if (!diag_skip(8, st))
+    bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
+                         rows, C, st);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
@@ -921,7 +922,8 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
-  bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
+  if (!diag_skip(8, st))
+    bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
