@@ -106,8 +106,9 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // Timing diagnostics, compiled only into the -DAVT_DIAG build (tools/build_variant.sh; avt_build_flags()
 // reports it and bench.py refuses it): AVT_DIAG_SKIP bit mask of launches to leave out of a captured graph
 // (1: forward bn_finalize, 2: backward bn finalize, 4: wgrad slab reduce, 8: backward BN reductions, 16: forward
-// bn_apply); results are WRONG when set.  Only the captured graph leaves them out: the eager warm-up steps fill the
-// accumulators / activations, so a replay runs on the previous step's (realistic) statistics and tensors.
+// bn_apply); results are WRONG when set.  Only the captured graph leaves them out.  The persistent BN accumulators
+// keep what the eager warm-up wrote (bits 2, 8: the replays run on realistic statistics); the tensors a skipped
+// launch would write inside the graph (bit 16) are graph-pool memory nobody wrote -- the data trap below.
 // Caveat, measured: the step's speed depends on the data -- a graph whose BN statistics are never written
 // normalises with uninitialised scale/shift, its activations collapse, and every MFMA kernel runs ~8-10 %
 // faster (power/clock), which reads as a spurious ~1 ms "cost" of the finalize launches at B=128
