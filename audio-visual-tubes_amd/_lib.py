@@ -67,6 +67,9 @@ SIGNATURES = {
     "avt_set_wgrad_row3": (_I, [_I, _I, _I]),
     "avt_set_halo3d": (_I, [_I]),
     "avt_set_halo_tps2": (_I, [_I]),
+    "avt_set_wgrad_fused": (_I, [_I, _I]),
+    "avt_conv2d_wgrad_tickets": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
+    "avt_conv2d_wgrad_tk": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P, _I, _P]),
     "avt_bn_acc_doubles": (_Z, [_L, _I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

@@ -1493,11 +1493,23 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
 
 template <int WM, int WN, int TM, int TN, int NST, int KG>
 static void launch_tn_one(dim3 grid, const GemmTNPipeParams& pp, hipStream_t st) {
-  hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG>), grid, dim3(WM * WN * 64 * KG), 0, st, pp);
+  if (pp.cnt != nullptr)
+    hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG, true>), grid, dim3(WM * WN * 64 * KG), 0, st, pp);
+  else
+    hipLaunchKernelGGL((conv_tn_pipe_kernel<WM, WN, TM, TN, NST, KG>), grid, dim3(WM * WN * 64 * KG), 0, st, pp);
+}
+
+// the wgrad plan's launch shape runs the fused in-kernel slab reduce (launch_tn_one; the deeper-ring A/B variants
+// keep the separate reduce)
+static bool tn_fusable(const WgradPlan& pl) {
+  if (!pl.pipe || pl.splits < 2) return false;
+  if (pl.BM == 256 && pl.BN == 256) return pl.nst < 4;
+  if (pl.BM == 256) return true;
+  return pl.kg == 2 || pl.nst < 6;
 }
 
 template <int CVEC, int BM, int BN>
-static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
+static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st, int* tickets = nullptr) {
   GemmTNParams p = pl.p;
   if (pl.pipe) {
     GemmTNPipeParams pp;
@@ -1507,6 +1519,9 @@ static void launch_tn(const WgradPlan& pl, float* slab, hipStream_t st) {
     pp.dy_bytes = (unsigned)((size_t)p.Kred * p.Mg * 2);
     pp.x_bytes = (unsigned)((size_t)(p.Kred / (p.P * p.Q)) * p.H * p.W * p.Cp * 2);
     pp.slab = slab;
+    pp.cnt = (slab != nullptr && tickets != nullptr && tn_fusable(pl)) ? tickets : nullptr;
+    pp.slab_bytes = (unsigned)pl.slab_bytes;
+    pp.splits = pl.splits;
     const dim3 grid(pl.tiles * pl.splits);
     if constexpr (BM == 256 && BN == 256) {
       if (pl.nst >= 5)
@@ -1757,6 +1772,38 @@ static StemWgradPlan stem_wgrad_plan(int N, int H, int W, int Cp, int Creal, int
 }
 }  // namespace avt
 
+// the fused slab reduce (conv_tn_pipe.h FUSED) for the tap-gather wgrads: avt_set_wgrad_fused / env AVT_WGRAD_FUSED
+// (1 default, 0 = the separate reduce launch), up to g_wgrad_fused_max_bytes of other splits' partials per tile (the
+// last block reads them alone: a deep split of a wide tile is reduced faster by the whole chip)
+static int g_wgrad_fused = -1;
+static long long g_wgrad_fused_max_bytes = -1;
+static bool wgrad_fused_plan(const WgradPlan& pl) {
+  if (g_wgrad_fused < 0) g_wgrad_fused = getenv("AVT_WGRAD_FUSED") ? atoi(getenv("AVT_WGRAD_FUSED")) : 1;
+  if (g_wgrad_fused_max_bytes < 0)
+    g_wgrad_fused_max_bytes = getenv("AVT_WGRAD_FUSED_MAX_KB") ? 1024LL * atoll(getenv("AVT_WGRAD_FUSED_MAX_KB"))
+                                                               : 2048LL * 1024;
+  return g_wgrad_fused && pl.slab_bytes > 0 && tn_fusable(pl) &&
+         (long long)(pl.splits - 1) * pl.BM * pl.BN * 4 <= g_wgrad_fused_max_bytes;
+}
+
+extern "C" int avt_set_wgrad_fused(int on, int max_kb) {
+  AVT_REQUIRE(on >= -1 && on <= 1, "avt_set_wgrad_fused: %d (0 separate reduce, 1 fused, -1 env AVT_WGRAD_FUSED)", on);
+  AVT_REQUIRE(max_kb >= -1, "avt_set_wgrad_fused: max_kb=%d", max_kb);
+  g_wgrad_fused = on;
+  g_wgrad_fused_max_bytes = max_kb < 0 ? -1 : 1024LL * max_kb;
+  return AVT_OK;
+}
+
+// tickets the fused wgrad slab reduce needs for this conv (avt_conv2d_wgrad_tk), 0: the shape does not use it
+extern "C" int avt_conv2d_wgrad_tickets(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride,
+                                        int pad) {
+  using namespace avt;
+  if (stem_wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad).grid > 0) return 0;
+  if (wgrad_halo_plan(N, H, W, Cp, Creal, K, R, S, stride, pad).ok) return 0;
+  const WgradPlan pl = wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
+  return wgrad_fused_plan(pl) ? pl.tiles : 0;
+}
+
 extern "C" size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride,
                                              int pad) {
   const StemWgradPlan sp = stem_wgrad_plan(N, H, W, Cp, Creal, K, R, S, stride, pad);
@@ -1769,9 +1816,22 @@ extern "C" size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Cr
 // dw += wgrad.  With a workspace of avt_conv2d_wgrad_workspace() bytes the split-K partials go
 // through an fp32 slab + one reduction pass (deterministic, 2x cheaper than atomics); without it
 // (or for the stems) they are added with fp32 atomics.  dw must hold zero or a gradient to add to.
+extern "C" int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
+                                   int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
+                                   int* tickets, int n_tickets, void* stream);
+
 extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
                                 int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
                                 void* stream) {
+  return avt_conv2d_wgrad_tk(x, dy, dw, N, H, W, Cp, Creal, K, R, S, stride, pad, workspace, ws_bytes, nullptr, 0,
+                             stream);
+}
+
+// tickets: >= avt_conv2d_wgrad_tickets() ints, zero on entry (the kernel leaves them zero), or null: the split-K slab
+// is summed by the last block of each tile instead of a separate reduce launch (same bits)
+extern "C" int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
+                                   int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
+                                   int* tickets, int n_tickets, void* stream) {
   AVT_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
   AVT_REQUIRE(K % 64 == 0, "conv2d_wgrad: K=%d must be a multiple of 64", K);
   AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
@@ -1810,19 +1870,22 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
   float* slab = (pl.slab_bytes > 0 && workspace != nullptr && ws_bytes >= pl.slab_bytes) ? (float*)workspace : nullptr;
   hipStream_t st = (hipStream_t)stream;
   const int BM = pl.BM, BN = pl.BN;
+  int* tk = (slab != nullptr && tickets != nullptr && n_tickets >= pl.tiles && Cp % 8 == 0 && wgrad_fused_plan(pl))
+                ? tickets
+                : nullptr;
   if (Cp == 4) {
     if (BM == 128) launch_tn<4, 128, 128>(pl, slab, st); else launch_tn<4, 64, 128>(pl, slab, st);
   } else if (Cp == 1) {
     if (BN == 128) launch_tn<1, 64, 128>(pl, slab, st); else launch_tn<1, 64, 64>(pl, slab, st);
   } else if (BM == 256) {
-    if (BN == 256) launch_tn<8, 256, 256>(pl, slab, st);
-    else launch_tn<8, 256, 128>(pl, slab, st);  // the plan pairs BM 256 with BN >= 128 only
+    if (BN == 256) launch_tn<8, 256, 256>(pl, slab, st, tk);
+    else launch_tn<8, 256, 128>(pl, slab, st, tk);  // the plan pairs BM 256 with BN >= 128 only
   } else if (BN == 128) {
-    if (BM == 128) launch_tn<8, 128, 128>(pl, slab, st); else launch_tn<8, 64, 128>(pl, slab, st);
+    if (BM == 128) launch_tn<8, 128, 128>(pl, slab, st, tk); else launch_tn<8, 64, 128>(pl, slab, st, tk);
   } else {
-    if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st); else launch_tn<8, 64, 64>(pl, slab, st);
+    if (BM == 128) launch_tn<8, 128, 64>(pl, slab, st, tk); else launch_tn<8, 64, 64>(pl, slab, st, tk);
   }
-  if (slab && !diag_skip(4, st)) {
+  if (slab && tk == nullptr && !diag_skip(4, st)) {
     // G waves per 64 slab positions: 1 where the positions alone give ~64 K threads, else up to min(splits, 16)
     const int wm = BM == 256 ? 4 : 2, wn = 2, tm = BM == 64 ? 1 : 2, tn = BN == 256 ? 4 : BN == 128 ? 2 : 1;
     const long long positions = (long long)pl.tiles * wm * wn * tm * tn * 4 * 64;

@@ -41,15 +41,7 @@ struct HaloArgs {
 #define HALO_DBG(bit) false
 #endif
 
-// write-through (sc1) 16-byte stores / loads of the split-K partial tiles: the hand-off of
-// MI355X_MICROARCH.md's table (sc1 stores, every storing wave's vmcnt(0), a barrier, one agent-scope
-// atomic add per workgroup; the last adder reads with sc1 loads) -- no L2 write-back fence needed
-__device__ __forceinline__ void store_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 16);
-}
-__device__ __forceinline__ f32x4 load_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-}
+// (store_wt16 / load_wt16, the write-through split-K hand-off: conv_nt_pipe.h)
 
 // LDS chunk swizzle of a 128-B row (8 16-B chunks): the 32x32x16 fragment reads (lanes 0-31 one chunk of 32
 // consecutive rows) are conflict-free with chunk ^ ((row >> 1) & 7) -- for ANY first row, which the tap shifts of

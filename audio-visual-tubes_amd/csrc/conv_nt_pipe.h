@@ -64,6 +64,16 @@ __device__ __forceinline__ void buf_lds16_at(__amdgpu_buffer_rsrc_t rs, unsigned
                : "memory");
 }
 
+// write-through (sc1) 16-byte stores / loads of the split-K partial tiles: the hand-off of
+// MI355X_MICROARCH.md's table (sc1 stores, every storing wave's vmcnt(0), a barrier, one agent-scope
+// atomic add per workgroup; the last adder reads with sc1 loads) -- no L2 write-back fence needed
+__device__ __forceinline__ void store_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, 16);
+}
+__device__ __forceinline__ f32x4 load_wt16(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
+
 __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, unsigned voff) {
   // the low 32 bits of a generic address into the LDS aperture are the LDS address (the aperture base is the high
   // word): a truncation, where a cast to the LDS address space would add a null check per load

@@ -19,6 +19,11 @@ struct GemmTNPipeParams {
   MagicDiv div_pq, div_q;
   unsigned dy_bytes, x_bytes;
   float* slab;  // non-null: store the split's partial tile to slab[split][Mg][R*S*C] (plain stores)
+  // FUSED: per-tile tickets (zero on entry, left zero) and the slab's bytes; the last block of a tile to take its
+  // ticket sums the tile's `splits` partials in split order into DW (no separate reduce launch)
+  int* cnt;
+  unsigned slab_bytes;
+  int splits;
 };
 
 template <int ROWB>
@@ -30,7 +35,10 @@ __device__ __forceinline__ int tn_swz(int row) {  // chunk XOR for a row of ROWB
 // KG = 2: two such wave groups per block split the block's k range in halves, each through its own LDS
 // ring, and meet in LDS at the end -- one partial tile per block instead of two (the split-K slab
 // traffic, which dominates the short-batch wgrads, halves at the same number of waves)
-template <int WM, int WN, int TM, int TN, int NST, int KG = 1>
+// FUSED: the split-K slab is reduced by the last block of each tile (write-through partial stores, one agent-scope
+// ticket per block, the last reads the partials back in split order -- the order wgrad_slab_reduce_native_kernel uses
+// with G = 1, so the two paths give the same bits); every block of the grid takes a ticket, an empty k range included
+template <int WM, int WN, int TM, int TN, int NST, int KG = 1, bool FUSED = false>
 __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNPipeParams pp) {
   constexpr int NW = WM * WN;  // waves per group
   static_assert(KG == 1 || KG == 2, "one or two k groups");
@@ -63,8 +71,11 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
   const int m0 = mt * BM, n0 = nt * BN;
   const int nkt_total = (p.Kred + 31) / 32;
   const int kb_begin = split * p.kt_per_split;
-  const int kb_end = min(nkt_total, kb_begin + p.kt_per_split);
-  if (kb_begin >= kb_end) return;
+  int kb_end = min(nkt_total, kb_begin + p.kt_per_split);
+  if (kb_begin >= kb_end) {
+    if constexpr (!FUSED) return;
+    kb_end = kb_begin;  // an empty range still stores a (zero) partial and takes its ticket
+  }
   // this group's half of the block's k range; both groups run `nkt` steps (the shorter one on
   // out-of-range dummy tiles, which load zeros), so the block-wide barriers pair up
   const int nkt = (kb_end - kb_begin + KG - 1) / KG;
@@ -247,7 +258,9 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
                 f32x4{acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2], acc[i][j][4 * q4 + 3]};
     }
     __syncthreads();
-    if (kgi == 1) return;
+    if (kgi == 1) {
+      if constexpr (!FUSED) return;
+    } else {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -258,6 +271,77 @@ __global__ __launch_bounds__(WM * WN * 64 * KG) void conv_tn_pipe_kernel(GemmTNP
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[i][j][4 * q4 + e] += o[e];
         }
+    }
+  }
+
+  if constexpr (FUSED) {
+    // the partial in register order, write-through (group 0's waves; group 1's accumulators were added above)
+    constexpr int PER_WAVE = TM * TN * 4 * 64;  // float4s per wave
+    constexpr int PER_TILE = NW * PER_WAVE;
+    const __amdgpu_buffer_rsrc_t rss = __builtin_amdgcn_make_buffer_rsrc((void*)pp.slab, (short)0, (int)pp.slab_bytes,
+                                                                         0x00020000);
+    if (kgi == 0) {
+      const unsigned base = (unsigned)(((split * ntiles + tile) * NW + wid) * PER_WAVE + lane) * 16u;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            store_wt16(rss, base + (unsigned)(((i * TN + j) * 4 + q) * 64 * 16),
+                       f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]});
+    }
+    wait_vmcnt<0>();  // this wave's partial has left for memory
+    __syncthreads();  // ... and every other wave's
+    int* flag = reinterpret_cast<int*>(smem_all);
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(pp.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (flag[0] != pp.splits - 1) return;  // not the last split of this tile (block-uniform)
+    if (tid == 0) pp.cnt[tile] = 0;        // ready for the next launch
+    // DW += sum over splits s = 0, 1, ... of the partials, every block thread on its own float4 positions, PU at a
+    // time with their split loads in flight together
+    constexpr int NTB = NW * 64 * KG, PU = 4;
+    const int ldw = p.R * p.S * p.Creal;
+    for (int f0 = tid; f0 < PER_TILE; f0 += NTB * PU) {
+      f32x4 a[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < pp.splits; s0 += 4) {
+        f32x4 v[4][PU];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int u = 0; u < PU; ++u) {
+            const int f = f0 + u * NTB;
+            v[k][u] = (s0 + k < pp.splits && f < PER_TILE)
+                          ? load_wt16(rss, (unsigned)((s0 + k) * ntiles + tile) * (unsigned)(PER_TILE * 16) +
+                                               (unsigned)f * 16u)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int u = 0; u < PU; ++u) a[u] += v[k][u];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int f = f0 + u * NTB;
+        if (f >= PER_TILE) continue;
+        // register-order position -> (wave, i, j, quarter, lane) -> DW rows r0 .. r0+3 of column col
+        const int ln = f & 63, qq = (f >> 6) & 3;
+        const int r = f >> 8;
+        const int jj = r % TN, ii = (r / TN) % TM, wv = r / (TN * TM);
+        const int wmv = wv / WN, wnv = wv % WN;
+        const int col = n0 + wnv * (BN / WN) + jj * 32 + (ln & 31);
+        const int r0 = m0 + wmv * (BM / WM) + ii * 32 + 8 * qq + 4 * (ln >> 5);
+        if (col < ldw) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (r0 + e < p.Mg) p.dw[(size_t)(r0 + e) * ldw + col] += a[u][e];
+        }
+      }
+    }
+    return;
   }
 
   // ---- epilogue: the partial tile to the slab in register order -- [split][tile][wave][i][j][quarter]

@@ -217,6 +217,9 @@ class _EngineStore(Store):
     def splitk(self, spec, dgrad, N, H, W):
         return self.e.splitk_ws(spec, dgrad, N, H, W)
 
+    def wgrad_tickets(self, spec, N, H, W):
+        return self.e.wgrad_tickets(spec, N, H, W)
+
 
 class AVEngine:
     """Two trunks + the hard-way head on one device."""
@@ -244,6 +247,9 @@ class AVEngine:
         self.splitk = os.environ.get("AVT_SPLITK", "0") != "0"
         self.split_pack = os.environ.get("AVT_SPLIT_PACK", "1") != "0"
         self._splitk_cnt: Dict = {}
+        # the wgrads' in-kernel split-K reduce (avt_conv2d_wgrad_tk): per call site and stream a persistent ticket
+        # array; AVT_WGRAD_FUSED=0 in the library turns the fused path off (the tickets are then 0 and unused)
+        self._wgrad_tk: Dict = {}
 
     def splitk_ws(self, spec, dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) for a split-K conv call (avt_conv2d_splitk_plan), or None: no split for the shape,
@@ -269,6 +275,19 @@ class AVEngine:
         if cnt is None:
             return None
         return torch.empty(nf, device=cnt.device, dtype=torch.float32), cnt
+
+    def wgrad_tickets(self, spec, N: int, H: int, W: int):
+        """Zeroed int32 tickets for this wgrad call (avt_conv2d_wgrad_tickets), allocated outside graph capture (the
+        engine runs an eager step before capturing; the kernel leaves them zero, so replays reuse them), or None."""
+        key = (spec.name, N, H, W, torch.cuda.current_stream().cuda_stream)
+        t = self._wgrad_tk.get(key)
+        if t is None:
+            n = int(query("avt_conv2d_wgrad_tickets", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+                          spec.stride, spec.pad))
+            if n == 0 or torch.cuda.is_current_stream_capturing():
+                return None
+            t = self._wgrad_tk[key] = torch.zeros(n, device=self.flat.flat.device, dtype=torch.int32)
+        return t
 
     def _side_stream(self):
         if self._side is None:

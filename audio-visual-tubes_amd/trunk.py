@@ -146,6 +146,11 @@ class Store:
         """(part, cnt) split-K workspace of this conv call (avt_conv2d_splitk_plan), or None."""
         return None
 
+    def wgrad_tickets(self, spec: "ConvSpec", N: int, H: int, W: int) -> Optional[torch.Tensor]:
+        """Persistent zeroed int32 tickets of this wgrad call site (avt_conv2d_wgrad_tickets; the kernel leaves
+        them zero), or None: the split-K slab then goes through the separate reduce launch."""
+        return None
+
 
 def _bn_finalize(c_out, acc, rows, bn: BNSpec, store: Store, training: bool, momentum=0.1, eps=1e-5, rep: int = 1):
     """BN statistics -> (scale, shift, mean, invstd) [4, C]; train mode also updates the running
@@ -349,9 +354,10 @@ class Trunk:
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
                         spec.stride, spec.pad))
         ws = torch.empty(wsb, device=x.device, dtype=torch.uint8) if wsb else None
+        tk = store.wgrad_tickets(spec, N, H, W) if ws is not None else None
         ev = ConvProfiler.begin()
-        call("avt_conv2d_wgrad", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
-             spec.stride, spec.pad, P(ws), wsb, stream_ptr())
+        call("avt_conv2d_wgrad_tk", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+             spec.stride, spec.pad, P(ws), wsb, P(tk), 0 if tk is None else tk.numel(), stream_ptr())
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
 

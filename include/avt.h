@@ -143,6 +143,14 @@ int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* ad
 size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad);
 int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
                      int S, int stride, int pad, void* workspace, size_t ws_bytes, void* stream);
+/* The same with the slab summed inside the wgrad kernel: the last block of each output tile to take its ticket adds
+ * the tile's split partials into dw in split order (the separate reduce's order: the same bits), so the reduce launch
+ * goes.  `tickets`: >= avt_conv2d_wgrad_tickets(...) ints, zero on entry, left zero (keep them for the next call);
+ * NULL or a count of 0: avt_conv2d_wgrad. */
+int avt_conv2d_wgrad_tickets(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad);
+int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
+                        int S, int stride, int pad, void* workspace, size_t ws_bytes, int* tickets, int n_tickets,
+                        void* stream);
 
 /* Input gradient of the 7x7 / stride 2 / pad 3 stem conv (base_models.py:135-138, the reference's autograd through
  * conv1 / conv1_a when the trunk input requires grad): gx[N][Cin][H][W] fp32 (NCHW, the input's layout) =

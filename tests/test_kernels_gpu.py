@@ -488,6 +488,52 @@ def test_conv_wgrad(case, slab, big, nst):
         assert torch.equal(dw, dw2)
 
 
+FUSED_WGRAD_CASES = CONV_CASES + [
+    # the 32-clip shard's layer2-4 and shortcut wgrads (the slab's split counts the fused reduce targets)
+    (32, 14, 14, 256, 256, 3, 1, 1), (32, 17, 19, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1),
+    (32, 28, 28, 128, 128, 3, 1, 1), (32, 28, 28, 128, 256, 1, 2, 0), (16, 14, 14, 256, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("tiles", [1, 0])
+@pytest.mark.parametrize("case", FUSED_WGRAD_CASES)
+def test_conv_wgrad_fused_reduce(case, tiles):
+    """avt_conv2d_wgrad_tk: the last block of each output tile sums the split partials into dw (write-through
+    partials, agent-scope tickets).  Against fp64, run twice (bitwise: the tickets are left zero and the summation order
+    is fixed), and against the separate reduce launch (avt_conv2d_wgrad): the same split order, so equal up to the
+    reduce's wave grouping of a few-tile slab (G > 1)."""
+    N, H, W, C, K, R, st, pad = case
+    Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+    xd, dyd = _rand_act(N, H, W, C, 12).relu().to(DEV), _rand_act(N, Pq, Qq, K, 13).to(DEV)
+    try:
+        call("avt_set_wgrad_tiles", tiles)
+        call("avt_set_wgrad_fused", 1, -1)
+        nt = int(query("avt_conv2d_wgrad_tickets", N, H, W, C, C, K, R, R, st, pad))
+        wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+        ws = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
+        tk = torch.zeros(max(nt, 1), device=DEV, dtype=torch.int32)
+        outs = []
+        for fused in (True, True, False):
+            dw = torch.full((K, R, R, C), 0.25, device=DEV)
+            call("avt_conv2d_wgrad_tk", P(xd), P(dyd), P(dw), N, H, W, C, C, K, R, R, st, pad, P(ws), wsb,
+                 P(tk) if fused else None, nt if fused else 0, S())
+            outs.append(dw)
+        torch.cuda.synchronize()
+    finally:
+        call("avt_set_wgrad_tiles", 1)
+        call("avt_set_wgrad_fused", -1, -1)
+    if N >= 8 and R == 3:
+        assert nt > 0, "the fused reduce should apply to this shape"
+    assert int(tk.abs().sum()) == 0, "tickets not left zero"
+    ref = torch.nn.grad.conv2d_weight(xd.cpu().double().permute(0, 3, 1, 2), (K, C, R, R),
+                                      dyd.cpu().double().permute(0, 3, 1, 2), stride=st, padding=pad)
+    assert rel_err(outs[0].permute(0, 3, 1, 2) - 0.25, ref) < 2e-4
+    assert torch.equal(outs[0], outs[1])
+    d = (outs[0] - outs[2]).abs().max().item()
+    print(f"{case} tiles={tiles} tickets={nt}: |fused - separate| = {d:.3e}")
+    assert d <= 1e-6 * outs[2].abs().max().item()
+
+
 def test_wgrad_large_splitk():
     # many pixels -> split-K with fp32 atomics
     N, H, W, C, K, R, st, pad = 8, 56, 56, 64, 64, 3, 1, 1
