@@ -493,6 +493,9 @@ FUSED_WGRAD_CASES = CONV_CASES + [
     (32, 14, 14, 256, 256, 3, 1, 1), (32, 17, 19, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1),
     (32, 28, 28, 128, 128, 3, 1, 1), (32, 28, 28, 128, 256, 1, 2, 0), (16, 14, 14, 256, 512, 3, 1, 1),
 ]
+# shapes whose plan takes the fused reduce (moderate split counts; a 256 x 256 tile split 14 ways reads 3.4 MB of
+# partials in its last block, past the 2 MB default bound, and keeps the separate reduce)
+FUSED_EXPECTED = {(32, 14, 14, 256, 256, 3, 1, 1), (32, 17, 19, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1)}
 
 
 @pytest.mark.parametrize("tiles", [1, 0])
@@ -522,7 +525,7 @@ def test_conv_wgrad_fused_reduce(case, tiles):
     finally:
         call("avt_set_wgrad_tiles", 1)
         call("avt_set_wgrad_fused", -1, -1)
-    if N >= 8 and R == 3:
+    if case in FUSED_EXPECTED:
         assert nt > 0, "the fused reduce should apply to this shape"
     assert int(tk.abs().sum()) == 0, "tickets not left zero"
     ref = torch.nn.grad.conv2d_weight(xd.cpu().double().permute(0, 3, 1, 2), (K, C, R, R),
