@@ -1772,13 +1772,15 @@ static StemWgradPlan stem_wgrad_plan(int N, int H, int W, int Cp, int Creal, int
 }
 }  // namespace avt
 
-// the fused slab reduce (conv_tn_pipe.h FUSED) for the tap-gather wgrads: avt_set_wgrad_fused / env AVT_WGRAD_FUSED
-// (1 default, 0 = the separate reduce launch), up to g_wgrad_fused_max_bytes of other splits' partials per tile (the
-// last block reads them alone: a deep split of a wide tile is reduced faster by the whole chip)
+// A/B knob: the fused slab reduce (conv_tn_pipe.h FUSED) for the tap-gather wgrads, avt_set_wgrad_fused / env
+// AVT_WGRAD_FUSED (0 default = the separate reduce launch; 1 = fused up to g_wgrad_fused_max_bytes of other splits'
+// partials per tile).  Bitwise equal where the separate reduce runs one wave per position, but SLOWER: the wgrad
+// family 355 -> 214 TF/s, the step -7 % at B=32 and -1.7 % at B=128 (profiles/r6_ab_wgrad_fused.txt) -- the
+// write-through partials and the last block's serial read of the other splits cost more than the reduce launch
 static int g_wgrad_fused = -1;
 static long long g_wgrad_fused_max_bytes = -1;
 static bool wgrad_fused_plan(const WgradPlan& pl) {
-  if (g_wgrad_fused < 0) g_wgrad_fused = getenv("AVT_WGRAD_FUSED") ? atoi(getenv("AVT_WGRAD_FUSED")) : 1;
+  if (g_wgrad_fused < 0) g_wgrad_fused = getenv("AVT_WGRAD_FUSED") ? atoi(getenv("AVT_WGRAD_FUSED")) : 0;
   if (g_wgrad_fused_max_bytes < 0)
     g_wgrad_fused_max_bytes = getenv("AVT_WGRAD_FUSED_MAX_KB") ? 1024LL * atoll(getenv("AVT_WGRAD_FUSED_MAX_KB"))
                                                                : 2048LL * 1024;

@@ -146,7 +146,8 @@ int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int
 /* The same with the slab summed inside the wgrad kernel: the last block of each output tile to take its ticket adds
  * the tile's split partials into dw in split order (the separate reduce's order: the same bits), so the reduce launch
  * goes.  `tickets`: >= avt_conv2d_wgrad_tickets(...) ints, zero on entry, left zero (keep them for the next call);
- * NULL or a count of 0: avt_conv2d_wgrad. */
+ * NULL or a count of 0: avt_conv2d_wgrad.  avt_conv2d_wgrad_tickets() is 0 unless avt_set_wgrad_fused(1) -- the fused
+ * form measured slower than the separate reduce (an A/B knob, include/avt_tuning.h). */
 int avt_conv2d_wgrad_tickets(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad);
 int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
                         int S, int stride, int pad, void* workspace, size_t ws_bytes, int* tickets, int n_tickets,

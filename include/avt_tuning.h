@@ -84,9 +84,9 @@ int avt_set_halo3d(int on);
  * and synchronises once per two taps (a 2-stage ring of two weight tiles) with waves 4-7 at s_setprio 1; -1: back to
  * the environment default.  Bitwise-equal results either way */
 int avt_set_halo_tps2(int on);
-/* avt_conv2d_wgrad_tk's in-kernel slab reduce: 1 (default, env AVT_WGRAD_FUSED) on where the other splits' partials of
- * a tile are at most max_kb KiB (env AVT_WGRAD_FUSED_MAX_KB, default 2048), 0 off (the separate reduce launch); -1:
- * back to the environment default */
+/* A/B knob, avt_conv2d_wgrad_tk's in-kernel slab reduce: 1 = on where the other splits' partials of a tile are at most
+ * max_kb KiB (env AVT_WGRAD_FUSED_MAX_KB, default 2048); 0 (default, env AVT_WGRAD_FUSED) = the separate reduce launch
+ * (measured faster); -1: back to the environment default */
 int avt_set_wgrad_fused(int on, int max_kb);
 /* 1 (default, env AVT_STEM): the 7x7/s2 stem forwards (C 4 or 1, K 64) run on the per-wave LDS-patch
  * stem kernel (BN statistics of the stored bf16 tensor, on the MFMA pipe); 0: the generic gather kernel */

@@ -501,7 +501,8 @@ FUSED_EXPECTED = {(32, 14, 14, 256, 256, 3, 1, 1), (32, 17, 19, 256, 256, 3, 1, 
 @pytest.mark.parametrize("tiles", [1, 0])
 @pytest.mark.parametrize("case", FUSED_WGRAD_CASES)
 def test_conv_wgrad_fused_reduce(case, tiles):
-    """avt_conv2d_wgrad_tk: the last block of each output tile sums the split partials into dw (write-through
+    """avt_conv2d_wgrad_tk (an A/B knob, avt_set_wgrad_fused(1); off by default: measured slower): the last block of
+    each output tile sums the split partials into dw (write-through
     partials, agent-scope tickets).  Against fp64, run twice (bitwise: the tickets are left zero and the summation order
     is fixed), and against the separate reduce launch (avt_conv2d_wgrad): the same split order, so equal up to the
     reduce's wave grouping of a few-tile slab (G > 1)."""
