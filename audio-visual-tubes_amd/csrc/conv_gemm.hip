@@ -1450,7 +1450,11 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   } else {
     int occ = max(1, 163840 / (pl.nst * 64 * (pl.BM + pl.BN)));
     if (pl.BM == 256 && pl.BN == 256) occ = 1;
-    const long long slots = (long long)num_cus() * occ;
+    // A/B (env AVT_WGRAD_SLOTS_PCT, default 100): the share of the chip's block slots the model assumes the wgrad has
+    // -- with both trunks' backward on two streams a wgrad shares the chip with the other trunk's kernels, and fewer
+    // splits mean fewer partials through the slab and a shorter reduce
+    static const int slots_pct = getenv("AVT_WGRAD_SLOTS_PCT") ? atoi(getenv("AVT_WGRAD_SLOTS_PCT")) : 100;
+    const long long slots = max(1LL, (long long)num_cus() * occ * slots_pct / 100);
     long long best = -1;
     splits = 1;
     for (int w = 1; w <= 4; ++w) {
