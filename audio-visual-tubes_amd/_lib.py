@@ -38,6 +38,13 @@ class BnBwdTarget(ctypes.Structure):
                 ("gc", ctypes.c_void_p), ("workspace", ctypes.c_void_p)]
 
 
+class SlabReduceDesc(ctypes.Structure):
+    """avt_slab_reduce_desc (include/avt.h): a wgrad split-K slab left for avt_wgrad_reduce_batch."""
+    _fields_ = [("slab", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("splits", ctypes.c_int), ("tiles", ctypes.c_int),
+                ("nnt", ctypes.c_int), ("Mg", ctypes.c_int), ("ldw", ctypes.c_int), ("wm", ctypes.c_int),
+                ("wn", ctypes.c_int), ("tm", ctypes.c_int), ("tn", ctypes.c_int)]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "avt_last_error": (ctypes.c_char_p, []),
@@ -70,6 +77,9 @@ SIGNATURES = {
     "avt_set_wgrad_fused": (_I, [_I, _I]),
     "avt_conv2d_wgrad_tickets": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I]),
     "avt_conv2d_wgrad_tk": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z, _P, _I, _P]),
+    "avt_conv2d_wgrad_defer": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _Z,
+                                    ctypes.POINTER(SlabReduceDesc), _P]),
+    "avt_wgrad_reduce_batch": (_I, [ctypes.POINTER(SlabReduceDesc), _I, _P]),
     "avt_bn_acc_doubles": (_Z, [_L, _I]),
     "avt_conv2d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_conv2d_dgrad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),

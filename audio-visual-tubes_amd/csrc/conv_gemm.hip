@@ -1495,6 +1495,56 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   return pl;
 }
 
+// Deferred split-K reduces, batched (avt_wgrad_reduce_batch): a trunk's wgrads leave their slabs (avt_conv2d_wgrad_defer)
+// and one launch sums all of them at the end of the trunk's backward segment -- blockIdx.y = the slab, a grid-stride
+// loop over its float4 positions; per position the splits in order, 8 loads in flight: the order of
+// wgrad_slab_reduce_native_kernel with G = 1, so the bits are the same as the per-wgrad reduce launches'.
+// (The reduces are off the backward's dgrad chain; at 32 clips per GPU their ~34 separate launches cost up to 7 % of
+// the step: profiles/r6_slab_skip.txt.)
+constexpr int kSlabBatch = 24;
+struct SlabReduceBatch {
+  int n;
+  avt_slab_reduce_desc e[kSlabBatch];
+};
+
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_batch_kernel(SlabReduceBatch b) {
+  const avt_slab_reduce_desc& E = b.e[blockIdx.y];
+  const int NW = E.wm * E.wn;
+  const long long per_tile = (long long)NW * E.tm * E.tn * 4 * 64;
+  const long long total = (long long)E.tiles * per_tile;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(E.slab);
+  const int BM = E.wm * E.tm * 32, BN = E.wn * E.tn * 32;
+  for (long long f = (long long)blockIdx.x * 256 + threadIdx.x; f < total; f += (long long)gridDim.x * 256) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < E.splits; s0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = s0 + i < E.splits ? s4[f + (s0 + i) * total] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += v[i];
+    }
+    const int lane = (int)(f & 63);
+    long long r = f >> 6;
+    const int q = (int)(r & 3);
+    r >>= 2;
+    const int jj = (int)(r % E.tn);
+    r /= E.tn;
+    const int i = (int)(r % E.tm);
+    r /= E.tm;
+    const int wid = (int)(r % NW);
+    const int tile = (int)(r / NW);
+    const int mt = tile / E.nnt, nt = tile - mt * E.nnt;
+    const int wm = wid / E.wn, wn = wid % E.wn;
+    const int col = nt * BN + wn * (BN / E.wn) + jj * 32 + (lane & 31);
+    const int r0 = mt * BM + wm * (BM / E.wm) + i * 32 + 8 * q + 4 * (lane >> 5);
+    if (col < E.ldw) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (r0 + e < E.Mg) E.dw[(size_t)(r0 + e) * E.ldw + col] += a[e];
+    }
+  }
+}
+
 template <int WM, int WN, int TM, int TN, int NST, int KG>
 static void launch_tn_one(dim3 grid, const GemmTNPipeParams& pp, hipStream_t st) {
   if (pp.cnt != nullptr)
@@ -1835,9 +1885,53 @@ extern "C" int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N,
 
 // tickets: >= avt_conv2d_wgrad_tickets() ints, zero on entry (the kernel leaves them zero), or null: the split-K slab
 // is summed by the last block of each tile instead of a separate reduce launch (same bits)
+static int conv2d_wgrad_impl(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K,
+                             int R, int S, int stride, int pad, void* workspace, size_t ws_bytes, int* tickets,
+                             int n_tickets, avt_slab_reduce_desc* defer, void* stream);
+
 extern "C" int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
                                    int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
                                    int* tickets, int n_tickets, void* stream) {
+  return conv2d_wgrad_impl(x, dy, dw, N, H, W, Cp, Creal, K, R, S, stride, pad, workspace, ws_bytes, tickets,
+                           n_tickets, nullptr, stream);
+}
+
+extern "C" int avt_conv2d_wgrad_defer(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal,
+                                      int K, int R, int S, int stride, int pad, void* workspace, size_t ws_bytes,
+                                      avt_slab_reduce_desc* desc, void* stream) {
+  AVT_REQUIRE(desc, "conv2d_wgrad_defer: null descriptor");
+  desc->splits = 0;
+  return conv2d_wgrad_impl(x, dy, dw, N, H, W, Cp, Creal, K, R, S, stride, pad, workspace, ws_bytes, nullptr, 0, desc,
+                           stream);
+}
+
+extern "C" int avt_wgrad_reduce_batch(const avt_slab_reduce_desc* descs, int n, void* stream) {
+  AVT_REQUIRE(n >= 0 && (n == 0 || descs), "wgrad_reduce_batch: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  for (int k0 = 0; k0 < n; k0 += kSlabBatch) {
+    SlabReduceBatch b{};
+    b.n = n - k0 < kSlabBatch ? n - k0 : kSlabBatch;
+    long long maxpos = 0;
+    for (int k = 0; k < b.n; ++k) {
+      const avt_slab_reduce_desc& d = descs[k0 + k];
+      AVT_REQUIRE(d.slab && d.dw && d.splits >= 1 && d.tiles >= 1 && d.nnt >= 1 && d.wm >= 1 && d.wn >= 1 &&
+                      d.tm >= 1 && d.tn >= 1,
+                  "wgrad_reduce_batch: descriptor %d is not from avt_conv2d_wgrad_defer", k0 + k);
+      b.e[k] = d;
+      const long long pos = (long long)d.tiles * d.wm * d.wn * d.tm * d.tn * 4 * 64;
+      maxpos = pos > maxpos ? pos : maxpos;
+    }
+    long long gx = (maxpos + 255) / 256;
+    if (gx > 1024) gx = 1024;
+    if (b.n > 0)
+      hipLaunchKernelGGL(wgrad_slab_reduce_batch_kernel, dim3((unsigned)gx, (unsigned)b.n), dim3(256), 0, st, b);
+  }
+  return check_launch("wgrad_reduce_batch");
+}
+
+static int conv2d_wgrad_impl(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K,
+                             int R, int S, int stride, int pad, void* workspace, size_t ws_bytes, int* tickets,
+                             int n_tickets, avt_slab_reduce_desc* defer, void* stream) {
   AVT_REQUIRE(x && dy && dw, "conv2d_wgrad: null pointer");
   AVT_REQUIRE(K % 64 == 0, "conv2d_wgrad: K=%d must be a multiple of 64", K);
   AVT_REQUIRE(Cp % 8 == 0 || Cp == 4 || Cp == 1, "conv2d_wgrad: C=%d unsupported", Cp);
@@ -1897,6 +1991,17 @@ extern "C" int avt_conv2d_wgrad_tk(const void* x, const void* dy, float* dw, int
     const long long positions = (long long)pl.tiles * wm * wn * tm * tn * 4 * 64;
     int G = 1;
     while (G * 2 <= pl.splits && G * 2 <= 16 && positions * G < 65536) G *= 2;
+    if (defer != nullptr && G == 1) {  // left for the batched reduce (the same order: G = 1)
+      defer->slab = slab;
+      defer->dw = dw;
+      defer->splits = pl.splits;
+      defer->tiles = pl.tiles;
+      defer->nnt = pl.p.Ng / BN;
+      defer->Mg = pl.p.Mg;
+      defer->ldw = R * S * Creal;
+      defer->wm = wm; defer->wn = wn; defer->tm = tm; defer->tn = tn;
+      return check_launch("conv2d_wgrad");
+    }
     const int nwb = G > 4 ? G : 4, ngrp = nwb / G;
     long long blocks = (positions + 64LL * ngrp - 1) / (64LL * ngrp);
     if (blocks > 4096) blocks = 4096;

@@ -220,6 +220,11 @@ class _EngineStore(Store):
     def wgrad_tickets(self, spec, N, H, W):
         return self.e.wgrad_tickets(spec, N, H, W)
 
+    pending: Optional[Dict[str, list]] = None  # trunk prefix -> deferred wgrad slabs (AVEngine.backward)
+
+    def wgrad_pending(self, prefix):
+        return None if self.pending is None else self.pending.get(prefix)
+
 
 class AVEngine:
     """Two trunks + the hard-way head on one device."""
@@ -250,6 +255,9 @@ class AVEngine:
         # the wgrads' in-kernel split-K reduce (avt_conv2d_wgrad_tk): per call site and stream a persistent ticket
         # array; AVT_WGRAD_FUSED=0 in the library turns the fused path off (the tickets are then 0 and unused)
         self._wgrad_tk: Dict = {}
+        # the wgrads' split-K slab reduces deferred to one batched launch per trunk and backward segment
+        # (avt_wgrad_reduce_batch; AVT_WGRAD_DEFER=0: a reduce launch per wgrad, the same bits)
+        self.defer_wgrad = os.environ.get("AVT_WGRAD_DEFER", "1") != "0"
 
     def splitk_ws(self, spec, dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) for a split-K conv call (avt_conv2d_splitk_plan), or None: no split for the shape,
@@ -573,11 +581,19 @@ class AVEngine:
             ga = torch.empty_like(a)
             call("avt_audio_pool_norm_bwd", P(gan), P(tape["an"]), P(tape["amax"]), P(tape["anorm"]), P(ga), B,
                  a.shape[1] * a.shape[2], C, stream_ptr())
-            return (yield from aud.backward_blocks_iter(ta, ga, self.store, hi, len(aud.blocks)))
+            r = yield from aud.backward_blocks_iter(ta, ga, self.store, hi, len(aud.blocks))
+            aud.flush_wgrad(self.store)  # the segment's deferred slab reduces, on the trunk's stream
+            return r
+
+        def img_hi_flushed():
+            r = yield from img.backward_blocks_iter(ti, gv, self.store, hi, len(img.blocks))
+            img.flush_wgrad(self.store)
+            return r
 
         def lo(tr, tp, g, pm):
             g, _ = yield from tr.backward_blocks_iter(tp, g, self.store, 0, hi, pm)
             yield from tr.backward_stem_iter(tp, g, self.store)
+            tr.flush_wgrad(self.store)
 
         def chain(tr, tp, first):
             g, pm = yield from first
@@ -585,8 +601,10 @@ class AVEngine:
             if on_trunk_end is not None:  # on the trunk's stream, behind its last gradient launch
                 on_trunk_end(tr)
 
+        if self.defer_wgrad:
+            self.store.pending = {img.prefix: [], aud.prefix: []}
         try:
-            img_hi = img.backward_blocks_iter(ti, gv, self.store, hi, len(img.blocks))
+            img_hi = img_hi_flushed()
             if seg:  # segment 1: layer4+layer3 of both trunks; boundary; segment 2: the rest
                 (ga, pa), (gv, pv) = self._interleave(audio_hi(), img_hi)
                 on_boundary((img.prefix + "hi", aud.prefix + "hi"))
@@ -594,8 +612,10 @@ class AVEngine:
                 on_boundary((img.prefix + "lo", aud.prefix + "lo"))
             else:
                 self._interleave(chain(aud, ta, audio_hi()), chain(img, ti, img_hi))
+            assert not self.store.pending or not any(self.store.pending.values()), "unflushed wgrad slabs"
         finally:
             self.store.grads = None
+            self.store.pending = None
 
 class TrunkEngine(AVEngine):
     """One ResNet-18 trunk called on its own (``model.imgnet(x)`` / a standalone ``resnet18(modal=...)``,

@@ -15,7 +15,7 @@ from typing import Dict, List, Optional
 
 import torch
 
-from ._lib import BnBwdTarget, DgradBnEpi, call, query
+from ._lib import BnBwdTarget, DgradBnEpi, SlabReduceDesc, call, query
 
 STAGES = [(64, 1), (128, 2), (256, 2), (512, 1)]
 # 1: BN-backward reductions fused into the dgrad epilogues (avt_conv2d_dgrad_bn); default 0: the separate
@@ -144,6 +144,11 @@ class Store:
 
     def splitk(self, spec: "ConvSpec", dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) split-K workspace of this conv call (avt_conv2d_splitk_plan), or None."""
+        return None
+
+    def wgrad_pending(self, prefix: str) -> Optional[list]:
+        """The list a trunk's deferred wgrad slab reduces go to (avt_conv2d_wgrad_defer; the engine sums them with one
+        avt_wgrad_reduce_batch at the end of each backward segment), or None: each wgrad reduces its own slab."""
         return None
 
     def wgrad_tickets(self, spec: "ConvSpec", N: int, H: int, W: int) -> Optional[torch.Tensor]:
@@ -354,12 +359,29 @@ class Trunk:
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
                         spec.stride, spec.pad))
         ws = torch.empty(wsb, device=x.device, dtype=torch.uint8) if wsb else None
-        tk = store.wgrad_tickets(spec, N, H, W) if ws is not None else None
+        pending = store.wgrad_pending(self.prefix) if ws is not None else None
+        tk = store.wgrad_tickets(spec, N, H, W) if ws is not None and pending is None else None
         ev = ConvProfiler.begin()
-        call("avt_conv2d_wgrad_tk", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
-             spec.stride, spec.pad, P(ws), wsb, P(tk), 0 if tk is None else tk.numel(), stream_ptr())
+        if pending is not None:
+            d = SlabReduceDesc()
+            call("avt_conv2d_wgrad_defer", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, P(ws), wsb, ctypes.byref(d), stream_ptr())
+            if d.splits > 0:
+                pending.append((d, ws))  # the workspace stays alive until the batched reduce
+        else:
+            call("avt_conv2d_wgrad_tk", P(x), P(gy), P(dw), N, H, W, spec.cp, spec.cin, spec.cout, spec.k, spec.k,
+                 spec.stride, spec.pad, P(ws), wsb, P(tk), 0 if tk is None else tk.numel(), stream_ptr())
         ConvProfiler.end(ev, "wgrad", 2.0 * gy.numel() * spec.k * spec.k * spec.cin,
                          2.0 * (x.numel() + gy.numel()) + 8.0 * dw.numel())
+
+    def flush_wgrad(self, store: Store):
+        """Sum this trunk's deferred wgrad slabs (one launch per 24) on the current stream."""
+        pending = store.wgrad_pending(self.prefix)
+        if not pending:
+            return
+        arr = (SlabReduceDesc * len(pending))(*[d for d, _ in pending])
+        call("avt_wgrad_reduce_batch", arr, len(pending), stream_ptr())
+        pending.clear()  # (stream-ordered reuse of the workspaces: allocated and freed on this stream)
 
     def _dgrad(self, gy, N, H, W, spec: ConvSpec, store: Store, add=None, inplace=False, epi=None, add_mask=None):
         """inplace: accumulate into `add` (dx = add + dgrad); a strided 1x1 conv then only touches the

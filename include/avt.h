@@ -143,6 +143,20 @@ int avt_conv2d_dgrad_bn(const void* dy, const void* wt, void* dx, const void* ad
 size_t avt_conv2d_wgrad_workspace(int N, int H, int W, int Cp, int Creal, int K, int R, int S, int stride, int pad);
 int avt_conv2d_wgrad(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K, int R,
                      int S, int stride, int pad, void* workspace, size_t ws_bytes, void* stream);
+/* Deferred split-K reduce: avt_conv2d_wgrad_defer runs the wgrad kernel and, where avt_conv2d_wgrad would launch its
+ * separate slab reduce (one wave per slab position), leaves it: *desc describes the slab (desc->splits > 0; keep the
+ * workspace alive) and dw is incomplete until avt_wgrad_reduce_batch(descs, n) sums any number of such slabs in one
+ * launch (blockIdx.y = the slab), in the same split order (the same bits).  desc->splits == 0: dw is complete. */
+typedef struct {
+  const float* slab;
+  float* dw;
+  int splits, tiles, nnt, Mg, ldw;
+  int wm, wn, tm, tn;  /* the wgrad tile's wave grid and 32x32 blocks per wave (register order of the partials) */
+} avt_slab_reduce_desc;
+int avt_conv2d_wgrad_defer(const void* x, const void* dy, float* dw, int N, int H, int W, int Cp, int Creal, int K,
+                           int R, int S, int stride, int pad, void* workspace, size_t ws_bytes, avt_slab_reduce_desc* desc,
+                           void* stream);
+int avt_wgrad_reduce_batch(const avt_slab_reduce_desc* descs, int n, void* stream);
 /* The same with the slab summed inside the wgrad kernel: the last block of each output tile to take its ticket adds
  * the tile's split partials into dw in split order (the separate reduce's order: the same bits), so the reduce launch
  * goes.  `tickets`: >= avt_conv2d_wgrad_tickets(...) ints, zero on entry, left zero (keep them for the next call);
