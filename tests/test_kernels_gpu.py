@@ -538,6 +538,45 @@ def test_conv_wgrad_fused_reduce(case, tiles):
     assert d <= 1e-6 * outs[2].abs().max().item()
 
 
+def test_wgrad_deferred_batched_reduce():
+    """avt_conv2d_wgrad_defer leaves each wgrad's slab (where its reduce would run one wave per position) and one
+    avt_wgrad_reduce_batch sums them all: bitwise equal to the per-wgrad reduce launches (the same split order), dw
+    untouched by the reduce until the batch runs, and more slabs than one launch takes (24) split over launches."""
+    from avt_amd._lib import SlabReduceDesc
+
+    shapes = [(32, 14, 14, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1), (32, 28, 28, 128, 128, 3, 1, 1),
+              (32, 28, 28, 128, 256, 1, 2, 0), (3, 14, 14, 256, 256, 3, 1, 1), (2, 17, 19, 512, 512, 3, 1, 1)] * 5
+    keep, descs, refs, outs = [], [], [], []
+    for n, (N, H, W, C, K, R, st, pad) in enumerate(shapes):
+        Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
+        xd, dyd = _rand_act(N, H, W, C, 40 + n).relu().to(DEV), _rand_act(N, Pq, Qq, K, 80 + n).to(DEV)
+        wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+        ws = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
+        ref = torch.full((K, R, R, C), 0.25, device=DEV)
+        call("avt_conv2d_wgrad", P(xd), P(dyd), P(ref), N, H, W, C, C, K, R, R, st, pad, P(ws), wsb, S())
+        torch.cuda.synchronize()
+        dw = torch.full((K, R, R, C), 0.25, device=DEV)
+        ws2 = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
+        d = SlabReduceDesc()
+        call("avt_conv2d_wgrad_defer", P(xd), P(dyd), P(dw), N, H, W, C, C, K, R, R, st, pad, P(ws2), wsb,
+             ctypes.byref(d), S())
+        keep += [xd, dyd, ws, ws2]
+        refs.append(ref)
+        outs.append(dw)
+        if d.splits > 0:
+            descs.append(d)
+    assert len(descs) > 24, len(descs)
+    torch.cuda.synchronize()
+    # before the batch: a deferred dw holds only the initial value
+    untouched = [o for o in outs if torch.all(o == 0.25)]
+    assert len(untouched) == len(descs)
+    arr = (SlabReduceDesc * len(descs))(*descs)
+    call("avt_wgrad_reduce_batch", arr, len(descs), S())
+    torch.cuda.synchronize()
+    for n, (o, r) in enumerate(zip(outs, refs)):
+        assert torch.equal(o, r), (n, shapes[n], (o - r).abs().max().item())
+
+
 def test_wgrad_large_splitk():
     # many pixels -> split-K with fp32 atomics
     N, H, W, C, K, R, st, pad = 8, 56, 56, 64, 64, 3, 1, 1
