@@ -256,8 +256,8 @@ class AVEngine:
         # array; AVT_WGRAD_FUSED=0 in the library turns the fused path off (the tickets are then 0 and unused)
         self._wgrad_tk: Dict = {}
         # the wgrads' split-K slab reduces deferred to one batched launch per trunk and backward segment
-        # (avt_wgrad_reduce_batch; AVT_WGRAD_DEFER=0: a reduce launch per wgrad, the same bits)
-        self.defer_wgrad = os.environ.get("AVT_WGRAD_DEFER", "1") != "0"
+        # (avt_wgrad_reduce_batch; AVT_WGRAD_DEFER=1 -- until measured, off: a reduce launch per wgrad, the same bits)
+        self.defer_wgrad = os.environ.get("AVT_WGRAD_DEFER", "0") != "0"
 
     def splitk_ws(self, spec, dgrad: bool, N: int, H: int, W: int):
         """(part, cnt) for a split-K conv call (avt_conv2d_splitk_plan), or None: no split for the shape,
