@@ -545,7 +545,7 @@ def test_wgrad_deferred_batched_reduce():
     from avt_amd._lib import SlabReduceDesc
 
     shapes = [(32, 14, 14, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1), (32, 28, 28, 128, 128, 3, 1, 1),
-              (32, 28, 28, 128, 256, 1, 2, 0), (3, 14, 14, 256, 256, 3, 1, 1), (2, 17, 19, 512, 512, 3, 1, 1)] * 5
+              (32, 28, 28, 128, 256, 1, 2, 0), (3, 14, 14, 256, 256, 3, 1, 1), (2, 17, 19, 512, 512, 3, 1, 1)] * 8  # 4 of the 6 shapes split K
     keep, descs, refs, outs = [], [], [], []
     for n, (N, H, W, C, K, R, st, pad) in enumerate(shapes):
         Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
