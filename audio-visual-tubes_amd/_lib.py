@@ -89,6 +89,7 @@ SIGNATURES = {
     "avt_conv2d_splitk_plan": (_I, [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P]),
     "avt_set_halo_splitk": (_I, [_I, _I]),
     "avt_set_wgrad_nst": (_I, [_I, _I]),
+    "avt_set_wgrad_slots_pct": (_I, [_I]),
     "avt_conv2d_fwd_ws": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
     "avt_conv2d_dgrad_ws": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _L, _P, _I, _P]),
     "avt_bn_apply_mask": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P]),

@@ -470,6 +470,7 @@ static int g_wgrad_slab_max = 1 << 30;
 static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epilogue) in k-tiles
 static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
+static int g_wgrad_slots_pct = -1;  // wgrad planner's slot share: 0 auto (by batch), 1-100 fixed, -1 env AVT_WGRAD_SLOTS_PCT
 static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel (conv_wgrad_halo.h): 0 off, 1 nine taps per
                                    // block, 2 one filter row per block, 3 (default) the one-row form for K = 64
@@ -646,6 +647,14 @@ extern "C" int avt_set_wgrad_nst(int nst, int nst_big) {
   AVT_REQUIRE(nst >= 4 && nst <= 8 && nst_big >= 3 && nst_big <= 5, "set_wgrad_nst: nst in 4..8, nst_big in 3..5");
   avt::g_wgrad_nst = nst;
   avt::g_wgrad_nst_big = nst_big;
+  return AVT_OK;
+}
+
+// share of the chip's block slots the tap-gather wgrad's split planner assumes: 0 auto (65 % at batch <= 32, 75 % at
+// <= 64, else 100 %), 1-100 fixed, -1 back to env AVT_WGRAD_SLOTS_PCT.  Size workspaces after changing it.
+extern "C" int avt_set_wgrad_slots_pct(int pct) {
+  AVT_REQUIRE(pct >= -1 && pct <= 100, "avt_set_wgrad_slots_pct: %d (0 auto, 1-100 fixed, -1 env)", pct);
+  avt::g_wgrad_slots_pct = pct;
   return AVT_OK;
 }
 
@@ -1450,10 +1459,13 @@ static WgradPlan wgrad_plan(int N, int H, int W, int Cp, int Creal, int K, int R
   } else {
     int occ = max(1, 163840 / (pl.nst * 64 * (pl.BM + pl.BN)));
     if (pl.BM == 256 && pl.BN == 256) occ = 1;
-    // A/B (env AVT_WGRAD_SLOTS_PCT, default 100): the share of the chip's block slots the model assumes the wgrad has
-    // -- with both trunks' backward on two streams a wgrad shares the chip with the other trunk's kernels, and fewer
-    // splits mean fewer partials through the slab and a shorter reduce
-    static const int slots_pct = getenv("AVT_WGRAD_SLOTS_PCT") ? atoi(getenv("AVT_WGRAD_SLOTS_PCT")) : 100;
+    // The share of the chip's block slots the model assumes the wgrad has: with both trunks' backward on two streams a
+    // wgrad shares the chip with the other trunk's kernels, and fewer splits mean fewer partials through the slab and
+    // a shorter reduce.  Auto (default): 65 % for a batch of <= 32, 75 % for <= 64, else 100 % -- measured same-box
+    // (profiles/r6_ab_wgrad_slots*.txt): 65 % is +3.3 % at B=32, 75 % +0.7 % at B=64, and 50 % -1.8 % at B=128.
+    // AVT_WGRAD_SLOTS_PCT / avt_set_wgrad_slots_pct fix it (1-100; 0 = auto).
+    if (g_wgrad_slots_pct < 0) g_wgrad_slots_pct = getenv("AVT_WGRAD_SLOTS_PCT") ? atoi(getenv("AVT_WGRAD_SLOTS_PCT")) : 0;
+    const int slots_pct = g_wgrad_slots_pct > 0 ? min(g_wgrad_slots_pct, 100) : N <= 32 ? 65 : N <= 64 ? 75 : 100;
     const long long slots = max(1LL, (long long)num_cus() * occ * slots_pct / 100);
     long long best = -1;
     splits = 1;

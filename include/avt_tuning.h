@@ -98,6 +98,10 @@ int avt_set_halo_splitk(int ksplit, int target_blocks);
 /* TN wgrad LDS ring depth: nst for the 4-wave tiles (4 default, 6, 8), nst_big for the 8-wave 256 x 256
  * tile (3 default, 4, 5) -- deeper rings keep more k-tiles in flight for a block alone on its CU */
 int avt_set_wgrad_nst(int nst, int nst_big);
+/* share of the chip's block slots the tap-gather wgrad's split-K planner assumes (the other trunk's kernels run
+ * beside it): 0 auto (65 at batch <= 32, 75 at <= 64, else 100), 1-100 fixed, -1 env AVT_WGRAD_SLOTS_PCT (unset:
+ * auto).  Workspace sizes follow the plan: query avt_conv2d_wgrad_workspace after changing it. */
+int avt_set_wgrad_slots_pct(int pct);
 
 #ifdef __cplusplus
 }

@@ -512,6 +512,7 @@ def test_conv_wgrad_fused_reduce(case, tiles):
     try:
         call("avt_set_wgrad_tiles", tiles)
         call("avt_set_wgrad_fused", 1, -1)
+        call("avt_set_wgrad_slots_pct", 100)  # FUSED_EXPECTED: the split counts of the whole-chip plan
         nt = int(query("avt_conv2d_wgrad_tickets", N, H, W, C, C, K, R, R, st, pad))
         wsb = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
         ws = torch.empty(max(wsb, 1), device=DEV, dtype=torch.uint8)
@@ -526,6 +527,7 @@ def test_conv_wgrad_fused_reduce(case, tiles):
     finally:
         call("avt_set_wgrad_tiles", 1)
         call("avt_set_wgrad_fused", -1, -1)
+        call("avt_set_wgrad_slots_pct", -1)
     if case in FUSED_EXPECTED:
         assert nt > 0, "the fused reduce should apply to this shape"
     assert int(tk.abs().sum()) == 0, "tickets not left zero"
@@ -538,6 +540,25 @@ def test_conv_wgrad_fused_reduce(case, tiles):
     assert d <= 1e-6 * outs[2].abs().max().item()
 
 
+def test_wgrad_slot_share_auto():
+    """The split planner's slot share (avt_set_wgrad_slots_pct): auto is 65 % of the chip's block slots at a batch of
+    <= 32, 75 % at <= 64 and 100 % above (the other trunk's kernels run beside a wgrad): the workspace (the plan's slab) of auto is the
+    fixed share's at each batch size; out-of-range shares are refused."""
+    shapes = [(14, 14, 512, 512, 3, 1, 1), (17, 19, 256, 256, 3, 1, 1), (28, 28, 128, 128, 3, 1, 1)]
+    try:
+        for H, W, C, K, R, st, pad in shapes:
+            ws = {}
+            for N in (32, 64, 128):
+                for pct in (0, 65, 75, 100):
+                    call("avt_set_wgrad_slots_pct", pct)
+                    ws[N, pct] = int(query("avt_conv2d_wgrad_workspace", N, H, W, C, C, K, R, R, st, pad))
+            assert ws[32, 0] == ws[32, 65] and ws[64, 0] == ws[64, 75] and ws[128, 0] == ws[128, 100], ws
+        with pytest.raises(RuntimeError):
+            call("avt_set_wgrad_slots_pct", 101)
+    finally:
+        call("avt_set_wgrad_slots_pct", -1)
+
+
 def test_wgrad_deferred_batched_reduce():
     """avt_conv2d_wgrad_defer leaves each wgrad's slab (where its reduce would run one wave per position) and one
     avt_wgrad_reduce_batch sums them all: bitwise equal to the per-wgrad reduce launches (the same split order), dw
@@ -547,6 +568,7 @@ def test_wgrad_deferred_batched_reduce():
     shapes = [(32, 14, 14, 256, 256, 3, 1, 1), (8, 14, 14, 512, 512, 3, 1, 1), (32, 28, 28, 128, 128, 3, 1, 1),
               (32, 28, 28, 128, 256, 1, 2, 0), (3, 14, 14, 256, 256, 3, 1, 1), (2, 17, 19, 512, 512, 3, 1, 1)] * 8  # 4 of the 6 shapes split K
     keep, descs, refs, outs = [], [], [], []
+    call("avt_set_wgrad_slots_pct", 100)  # the whole-chip plan's split counts (4 of the 6 shapes split)
     for n, (N, H, W, C, K, R, st, pad) in enumerate(shapes):
         Pq, Qq = conv_out(H, R, st, pad), conv_out(W, R, st, pad)
         xd, dyd = _rand_act(N, H, W, C, 40 + n).relu().to(DEV), _rand_act(N, Pq, Qq, K, 80 + n).to(DEV)
@@ -565,6 +587,7 @@ def test_wgrad_deferred_batched_reduce():
         outs.append(dw)
         if d.splits > 0:
             descs.append(d)
+    call("avt_set_wgrad_slots_pct", -1)
     assert len(descs) > 24, len(descs)
     torch.cuda.synchronize()
     # before the batch: a deferred dw holds only the initial value
