@@ -1021,7 +1021,11 @@ static void launch_c64(const GemmNTParams& p, hipStream_t st) {
     }
   // as few blocks as the same number of tile rounds needs (1568 vision tiles at B=128: 7 rounds on 224
   // blocks, not 6.1 on 256): the CUs left over take the other trunk's concurrent kernels
-  const int rounds = (ca.tiles + num_cus() - 1) / num_cus();
+  // (A/B, env AVT_C64_SHARE, default 100: the share of the CUs the persistent grid may take -- the rest run the
+  // other trunk's kernels)
+  static const int c64_share = getenv("AVT_C64_SHARE") ? atoi(getenv("AVT_C64_SHARE")) : 100;
+  const int cus = max(1, num_cus() * min(max(c64_share, 1), 100) / 100);
+  const int rounds = (ca.tiles + cus - 1) / cus;
   const int grid = rounds > 0 ? (ca.tiles + rounds - 1) / rounds : 0;
   if (grid <= 0) return;
   // 8-wave blocks (two waves per SIMD; default): layer-1 fwd/dgrad 519/630 -> 638/762 TFLOP/s (vision), step
@@ -1720,7 +1724,9 @@ static WgradHaloPlan wgrad_halo_plan(int N, int H, int W, int Cp, int Creal, int
   if (best < 0) return pl;
   a.nkt = N * a.tiles_img;
   const int per_split = (K / BM) * (Cp / 64) * (pl.row3 ? 3 : 1);
-  const long long slots = (long long)num_cus() * per_cu;
+  // (A/B, env AVT_WGRAD_HALO_SHARE, default 100: the share of the chip's block slots the split count assumes)
+  static const int halo_share = getenv("AVT_WGRAD_HALO_SHARE") ? atoi(getenv("AVT_WGRAD_HALO_SHARE")) : 100;
+  const long long slots = max(1LL, (long long)num_cus() * per_cu * min(max(halo_share, 1), 100) / 100);
   int splits = (int)(slots / per_split);
   if (pl.row3) {  // at least row3_min_kt() k-tiles per split: the slab (splits x 147 KB at K 64) is the cost at small N
     const int cap = a.nkt / row3_min_kt();
