@@ -471,7 +471,7 @@ static int g_wgrad_wave_cost = 16; // per-block fixed cost (prologue fill + epil
 static int g_wgrad_big = -1;       // allow the 8-wave 256-wide wgrad tiles (-1: env AVT_WGRAD_BIG, default 1)
 static int g_wgrad_nst = -1, g_wgrad_nst_big = -1;  // TN ring depth (4-wave / 8-wave tiles); -1: env
 static int g_wgrad_slots_pct = -1;  // wgrad planner's slot share: 0 auto (by batch), 1-100 fixed, -1 env AVT_WGRAD_SLOTS_PCT
-static int g_small_tile_waves = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile; -2: env)
+static int g_small_tile_pct = -2;  // 64-row fwd/dgrad tiles for small GEMMs (use_small_tile): % of the CUs; -2: env
 static int g_wgrad_halo = -1;      // 3x3/s1 wgrad on the halo kernel (conv_wgrad_halo.h): 0 off, 1 nine taps per
                                    // block, 2 one filter row per block, 3 (default) the one-row form for K = 64
                                    // (layer 1: 480-550 -> 670-715 TFLOP/s), tap-gather elsewhere; -1 = env AVT_WGRAD_HALO
@@ -633,7 +633,8 @@ extern "C" int avt_set_stem_kernel(int on) {
 }
 
 extern "C" int avt_set_small_tiles(int waves) {
-  avt::g_small_tile_waves = waves;
+  AVT_REQUIRE(waves >= -2 && waves <= 64, "avt_set_small_tiles: %d (blocks per CU; 0 never, -1 always, -2 env)", waves);
+  avt::g_small_tile_pct = waves > 0 ? 100 * waves : waves;
   return AVT_OK;
 }
 
@@ -824,19 +825,24 @@ static bool halo_eligible(const GemmNTParams& p) {
 
 // Small GEMMs (a few clips per GPU: BASELINE configs[2] runs 32 per GPU): a tile grid that leaves
 // most of the 256 CUs idle loses more than a smaller tile's lower reuse costs.  Rows per tile drop
-// from 128 to 64 when the 128-row grid would not give every CU `g_small_tile_waves` block(s)
-// (0 = never; env AVT_SMALL_TILES overrides the default 1, -1 = always).  Measured per shape
-// (tools/conv_bench.py --small): a 128-row grid of fewer blocks than CUs runs faster on 64-row tiles
-// (e.g. B=32 layer3 263 -> 354 TFLOP/s), one of 1-2 blocks per CU does not (B=32 audio layer4 769 -> 541).
+// from 128 to 64 when the 128-row grid would not give g_small_tile_pct % of the CUs a block.
+// Measured per shape (tools/conv_bench.py --small): a 128-row grid of fewer blocks than CUs runs faster alone on
+// 64-row tiles (e.g. B=32 layer3 263 -> 354 TFLOP/s), one of 1-2 blocks per CU does not (B=32 audio layer4 769 ->
+// 541).  In the step the other trunk's kernels take the CUs a 128-row grid leaves: at 100 % (rounds 2-5) the
+// 64-row tiles lost 1.6 % at B=32 and 0.5 % at B=64 against none, and gained 2.2 % on the tube step's 8-clip audio
+// trunk (profiles/r6_ab_small_tiles*.txt); the default is AVT_SMALL_TILES_PCT (50).  avt_set_small_tiles(w) / env
+// AVT_SMALL_TILES = w blocks per CU (100 w %), 0 never, -1 always.
 static bool use_small_tile(const GemmNTParams& p, int BN) {
-  if (g_small_tile_waves == -2) {
+  if (g_small_tile_pct == -2) {
     const char* e = getenv("AVT_SMALL_TILES");
-    g_small_tile_waves = e ? atoi(e) : 1;
+    const char* ep = getenv("AVT_SMALL_TILES_PCT");
+    const int w = e ? atoi(e) : 1;
+    g_small_tile_pct = e ? (w > 0 ? 100 * w : w) : ep ? atoi(ep) : 50;
   }
-  if (g_small_tile_waves == 0) return false;
-  if (g_small_tile_waves < 0) return true;
+  if (g_small_tile_pct == 0) return false;
+  if (g_small_tile_pct < 0) return true;
   const long long blocks128 = (long long)((p.M + 127) / 128) * (p.Ng / BN);
-  return blocks128 < (long long)g_small_tile_waves * num_cus();
+  return blocks128 * 100 < (long long)g_small_tile_pct * num_cus();
 }
 
 template <int MODE, int WM, int WN, int TM, int TN, int NSTB, int PRMAX, bool EPI, int OPT = 0>

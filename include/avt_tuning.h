@@ -55,8 +55,8 @@ int avt_set_s2_dgrad_one(int on);
  * 5: 256x128 8 waves k64/2, 6: 256x128 8 waves k32/3) */
 int avt_set_nt128_config(int cfg);
 /* fwd/dgrad tiles of 64 rows (64x128 / 64x64; a 64x128 halo tile for layer3/4) when the 128-row tile
- * grid would give fewer than `waves` blocks per CU (small per-GPU batches); 0 = never, -1 = always;
- * default 1 (env AVT_SMALL_TILES) */
+ * grid would give fewer than `waves` blocks per CU (small per-GPU batches); 0 = never, -1 = always, -2 = back to
+ * the environment: AVT_SMALL_TILES (blocks per CU) or AVT_SMALL_TILES_PCT (% of the CUs; default 50) */
 int avt_set_small_tiles(int waves);
 /* wgrad split-K policy: target_blocks 0 = wave model (default), >0 = about that many blocks in total;
  * at least min_ktiles 32-pixel tiles per block */

@@ -111,7 +111,7 @@ def tiles(request):
     """Run with the 128-row fwd/dgrad tiles, then with the 64-row small-batch tiles (avt_set_small_tiles)."""
     call("avt_set_small_tiles", request.param)
     yield request.param
-    call("avt_set_small_tiles", 1)
+    call("avt_set_small_tiles", -2)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -262,7 +262,7 @@ def test_halo_stages_bitwise_equal(case):
                 torch.testing.assert_close(o[2], outs[0][2], rtol=1e-9, atol=1e-6)
     finally:
         call("avt_set_halo_stages", 2, 3)
-        call("avt_set_small_tiles", 1)
+        call("avt_set_small_tiles", -2)
         call("avt_set_halo8", -1)
 
 
@@ -1070,7 +1070,7 @@ def test_conv_dgrad_bn_epilogue(case, mode):
         _dgrad_bn_epilogue(case, mode)
     finally:
         call("avt_set_c64", 1)
-        call("avt_set_small_tiles", 1)
+        call("avt_set_small_tiles", -2)
 
 
 def _dgrad_bn_epilogue(case, mode):

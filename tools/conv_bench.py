@@ -116,7 +116,7 @@ def main():
                                          pad, S()))
                 line += f" dgrad {flops / ms / 1e9:6.0f}"
                 tot[(f"dgrad_small{sv}", 1)] = tot.get((f"dgrad_small{sv}", 1), 0) + ms
-            call("avt_set_small_tiles", 2)
+            call("avt_set_small_tiles", -2)
         if args.stages and R == 3 and st == 1:
             for pair in args.stages.split(";"):
                 call("avt_set_halo_stages", *(int(v) for v in pair.split(",")))
