@@ -100,6 +100,7 @@ SIGNATURES = {
     "avt_bn_finalize_rep": (_I, [_P, _L, _L, _I, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P]),
     "avt_conv3d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_video_stem_im2col": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "avt_maxpool3d_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
     "avt_pack_conv3d_weight": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "avt_repeat_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),
     "avt_sum_rep_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),

@@ -100,6 +100,64 @@ __global__ __launch_bounds__(256) void sum_rep_rows_kernel(const float* __restri
   }
 }
 
+// MaxPool3d(kernel_size=3, stride=2, padding=1) (resnet3D.py:129, applied after the stem's BN + ReLU when
+// no_max_pool=False, :200-201) over bf16 NDHWC [N][T][H][W][C] -> [N][To][Ho][Wo][C], To = (T - 1) / 2 + 1 (same
+// for H, W).  One thread per output pixel and 8 channels (16 B loads of the 27 taps); taps outside the clip are
+// skipped (torch's -inf padding); the result is the winning input's bits, and a NaN tap wins, as in max_pool3d.
+__global__ __launch_bounds__(256) void maxpool3d_k3s2p1_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                               int N, int T, int H, int W, int C, int To, int Ho,
+                                                               int Wo) {
+  const int cv = C / 8;
+  const long long total = (long long)N * To * Ho * Wo * cv;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % cv);
+    long long r = i / cv;
+    const int wo = (int)(r % Wo);
+    r /= Wo;
+    const int ho = (int)(r % Ho);
+    r /= Ho;
+    const int to = (int)(r % To);
+    const int n = (int)(r / To);
+    float m[8];
+    unsigned short bits[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      m[e] = -__builtin_inff();
+      bits[e] = 0xff80;  // -inf (never stored: every window holds at least its centre tap)
+    }
+    for (int dt = 0; dt < 3; ++dt) {
+      const int t = 2 * to - 1 + dt;
+      if (t < 0 || t >= T) continue;
+      for (int dh = 0; dh < 3; ++dh) {
+        const int h = 2 * ho - 1 + dh;
+        if (h < 0 || h >= H) continue;
+        for (int dw = 0; dw < 3; ++dw) {
+          const int w = 2 * wo - 1 + dw;
+          if (w < 0 || w >= W) continue;
+          const u32x4 v = reinterpret_cast<const u32x4*>(x)[(((long long)n * T + t) * H + h) * (long long)W * cv +
+                                                           (long long)w * cv + c8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const unsigned short b = (unsigned short)((e & 1) ? (v[e >> 1] >> 16) : (v[e >> 1] & 0xffff));
+            const float f = bf2f(b);
+            if (f > m[e] || f != f) {
+              if (m[e] == m[e]) {  // a NaN already taken stays
+                m[e] = f;
+                bits[e] = b;
+              }
+            }
+          }
+        }
+      }
+    }
+    u32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (unsigned)bits[2 * q] | ((unsigned)bits[2 * q + 1] << 16);
+    reinterpret_cast<u32x4*>(y)[i] = o;
+  }
+}
+
 static int grid_for(long long n) {
   long long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -132,6 +190,19 @@ extern "C" int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, i
   hipLaunchKernelGGL(pack_conv3d_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)out, K,
                      C, KT, R, S, fold, total);
   return check_launch("pack_conv3d_weight");
+}
+
+// x bf16 [N][T][H][W][C] (C % 8 == 0) -> y bf16 [N][(T-1)/2+1][(H-1)/2+1][(W-1)/2+1][C]: nn.MaxPool3d(3, 2, 1)
+extern "C" int avt_maxpool3d_fwd(const void* x, void* y, int N, int T, int H, int W, int C, void* stream) {
+  AVT_REQUIRE(x && y, "maxpool3d_fwd: null pointer");
+  AVT_REQUIRE(N >= 0 && T >= 1 && H >= 1 && W >= 1 && C >= 8 && C % 8 == 0,
+              "maxpool3d_fwd: N=%d T=%d H=%d W=%d C=%d (C a multiple of 8)", N, T, H, W, C);
+  const int To = (T - 1) / 2 + 1, Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const long long n = (long long)N * To * Ho * Wo * (C / 8);
+  if (n == 0) return AVT_OK;
+  hipLaunchKernelGGL(maxpool3d_k3s2p1_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (bf16_t*)y, N, T, H, W, C, To, Ho, Wo);
+  return check_launch("maxpool3d_fwd");
 }
 
 // Audio de-duplication of the tube step (train_3D.py:128-130 repeats each clip's spectrogram t

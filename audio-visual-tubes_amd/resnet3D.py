@@ -5,7 +5,7 @@ n_classes=1039)`` (model.py:20; resnet3D.py:103-234), so ``torch.manual_seed(s)`
 reference's weights and ``state_dict`` keys/shapes match (``vidnet.conv1.weight`` [64,3,7,7,7],
 ``vidnet.layerL.B.downsample.{0,1}.*``, ``vidnet.fc.*``).  Inside FullModel the compute runs in its
 engine (tube.py); called on its own (``FullModel.vidnet(video)`` or a standalone
-``generate_model(18, no_max_pool=True, ...)``) the same kernels run through tube.R3DEngine and return
+``generate_model(18, ...)``, with the stem max-pool or without) the same kernels run through tube.R3DEngine and return
 the ``fc`` logits as resnet3D.ResNet.forward does (resnet3D.py:197-213).  Forward only: the build
 computes no gradients for the video trunk (FullModel detaches it), so a call that would need them raises.
 """
@@ -116,9 +116,6 @@ class ResNet(nn.Module):
         """resnet3D.ResNet.forward (resnet3D.py:197-213): x fp32 [b,3,t,H,W] -> fc logits [b, n_classes]."""
         from .tube import R3DEngine
 
-        if not self.no_max_pool:
-            raise NotImplementedError("avt: the R3D stem max-pool is not built (FullModel uses no_max_pool=True, "
-                                      "model.py:20)")
         if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters())):
             raise NotImplementedError("avt: the R3D trunk is forward-only in this build (FullModel detaches it); "
                                       "call it under torch.no_grad() or with requires_grad_(False) parameters")
@@ -130,7 +127,7 @@ class ResNet(nn.Module):
         else:
             prefix, flat = "", self._flat_store()
         if self._avt_engine is None or self._avt_engine.flat is not flat:
-            self._avt_engine = R3DEngine(flat, prefix)
+            self._avt_engine = R3DEngine(flat, prefix, max_pool=not self.no_max_pool)
         return self._avt_engine.forward(x, self.training)
 
 

@@ -65,10 +65,12 @@ class Conv3dSpec:
 
 
 class R3DTrunk:
-    """resnet3D ResNet(BasicBlock, [2,2,2,2], no_max_pool=True) up to layer4, forward only."""
+    """resnet3D ResNet(BasicBlock, [2,2,2,2]) up to layer4, forward only; no_max_pool=True (FullModel, model.py:20)
+    unless max_pool (the stem's MaxPool3d(3, 2, 1), resnet3D.py:129, 200-201)."""
 
-    def __init__(self, prefix: str):
+    def __init__(self, prefix: str, max_pool: bool = False):
         self.prefix = prefix
+        self.max_pool = max_pool
         self.stem = Conv3dSpec(prefix + "conv1.weight", 3, 64, 7, 7, 2, 3, 3, stem=True)
         self.bn1 = BNSpec(prefix + "bn1", 64)
         self.blocks = []
@@ -141,6 +143,11 @@ class R3DTrunk:
         h = torch.empty_like(c0)
         call("avt_bn_apply", P(c0), P(s0[0]), P(s0[1]), None, None, None, P(h), rows, 64, 1, stream_ptr())
         del c0
+        if self.max_pool:  # resnet3D.py:200-201
+            To, Ho, Wo = (T - 1) // 2 + 1, (H - 1) // 2 + 1, (W - 1) // 2 + 1
+            hp = torch.empty(b * To, Ho, Wo, 64, device=h.device, dtype=torch.bfloat16)
+            call("avt_maxpool3d_fwd", P(h), P(hp), b, T, H, W, 64, stream_ptr())
+            h, T, H, W = hp, To, Ho, Wo
         for blk in self.blocks:
             c1, s1, Ho, Wo = self._conv(h, b, T, H, W, blk["conv1"], blk["bn1"], store, training)
             h1 = torch.empty_like(c1)
@@ -302,8 +309,9 @@ class R3DEngine(AVEngine):
     layer4 on libavt as inside FullModel (R3DTrunk), then AdaptiveAvgPool3d((1,1,1)) + fc on the pooled
     fp32 features.  Forward only, as everywhere in this build (FullModel detaches the video trunk)."""
 
-    def __init__(self, flat: FlatStore, prefix: str):
+    def __init__(self, flat: FlatStore, prefix: str, max_pool: bool = False):
         self._prefix = prefix
+        self._max_pool = max_pool
         super().__init__(flat)
         self.concurrent = False
         self.store = _TubeStore(self)
@@ -311,7 +319,7 @@ class R3DEngine(AVEngine):
                                      device=flat.flat.device, dtype=torch.long)
 
     def _setup_trunks(self):
-        self.vid = R3DTrunk(self._prefix)
+        self.vid = R3DTrunk(self._prefix, self._max_pool)
         self.packs3d: Dict[str, torch.Tensor] = {}
         self.trunks2d = []
         self.bn_trunks = [self.vid]

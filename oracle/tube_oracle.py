@@ -114,10 +114,13 @@ def _bn3(x, sd, prefix, training):
     return orc._bn(x, sd, prefix, training)
 
 
-def r3d18_forward(sd, prefix: str, x: torch.Tensor, training: bool = True) -> torch.Tensor:
-    """resnet3D.ResNet.forward up to layer4 (resnet3D.py:196-206). x [b,3,t,H,W] -> [b,512,t,h,w]."""
+def r3d18_forward(sd, prefix: str, x: torch.Tensor, training: bool = True, max_pool: bool = False) -> torch.Tensor:
+    """resnet3D.ResNet.forward up to layer4 (resnet3D.py:196-206). x [b,3,t,H,W] -> [b,512,t,h,w].  max_pool: the
+    stem's nn.MaxPool3d(kernel_size=3, stride=2, padding=1) of no_max_pool=False (resnet3D.py:129, 200-201)."""
     x = F.conv3d(x, sd[prefix + "conv1.weight"], stride=(1, 2, 2), padding=(3, 3, 3))
     x = F.relu(_bn3(x, sd, prefix + "bn1", training))
+    if max_pool:
+        x = F.max_pool3d(x, kernel_size=3, stride=2, padding=1)
     for li, (planes, stride) in enumerate(R3D_STAGES, start=1):
         for bi in range(2):
             s = stride if bi == 0 else 1

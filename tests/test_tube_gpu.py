@@ -421,10 +421,36 @@ def test_hardway_attention_standalone_autograd(b, t, hw, C, normalized):
     assert rel_err(ad.grad, ar.grad) < 2e-4
 
 
-@pytest.mark.parametrize("standalone", [False, True])
-def test_r3d_forward_standalone(standalone):
-    """VERDICT r3 Missing #3: FullModel.vidnet(video) / a standalone generate_model(18, no_max_pool=True,
-    n_classes=1039)(video) return resnet3D.ResNet.forward's fc logits (resnet3D.py:197-213: layer4 ->
+@pytest.mark.parametrize("shape", [(2, 16, 112, 112, 64), (1, 5, 7, 9, 8), (3, 1, 1, 2, 16), (2, 4, 6, 6, 64)])
+def test_maxpool3d_matches_torch(shape):
+    """avt_maxpool3d_fwd = nn.MaxPool3d(kernel_size=3, stride=2, padding=1) (resnet3D.py:129) on NDHWC bf16: bitwise
+    equal to torch's max_pool3d of the same values (a max of bf16 values is exact), odd and unit extents, NaN and
+    -0.0 / +0.0 ties (the first tap wins, as in torch)."""
+    N, T, H, W, C = shape
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, T, H, W, C, generator=g).to(torch.bfloat16)
+    x[..., 0] = torch.where(torch.rand(N, T, H, W, generator=g) < 0.5, torch.tensor(-0.0), torch.tensor(0.0)).bfloat16()
+    if x.numel() > 64:
+        x.view(-1)[37] = float("nan")
+    To, Ho, Wo = (T - 1) // 2 + 1, (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    xd = x.to(DEV)
+    y = torch.full((N, To, Ho, Wo, C), 7.0, device=DEV, dtype=torch.bfloat16)
+    call("avt_maxpool3d_fwd", P(xd), P(y), N, T, H, W, C, S())
+    ref = F.max_pool3d(x.float().permute(0, 4, 1, 2, 3).contiguous(), kernel_size=3, stride=2, padding=1)
+    ref = ref.permute(0, 2, 3, 4, 1).to(torch.bfloat16)
+    got = y.cpu()
+    assert got.shape == ref.shape
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16)) or (
+        torch.equal(torch.isnan(got), torch.isnan(ref)) and
+        torch.equal(got.nan_to_num().view(torch.int16), ref.nan_to_num().view(torch.int16)))
+    with pytest.raises(RuntimeError):
+        call("avt_maxpool3d_fwd", P(xd), P(y), N, T, H, W, 12, S())
+
+
+@pytest.mark.parametrize("standalone,max_pool", [(False, False), (True, False), (True, True)])
+def test_r3d_forward_standalone(standalone, max_pool):
+    """VERDICT r3 Missing #3: FullModel.vidnet(video) / a standalone generate_model(18, no_max_pool=True or False
+    (the stem max-pool, VERDICT r5 gap 3), n_classes=1039)(video) return resnet3D.ResNet.forward's fc logits (resnet3D.py:197-213: layer4 ->
     AdaptiveAvgPool3d -> fc) on the same kernels, vs the fp64 restatement; forward-only (raises where
     gradients would be needed)."""
     from avt_amd.resnet3D import generate_model
@@ -432,7 +458,7 @@ def test_r3d_forward_standalone(standalone):
     video = tor.make_video(2, 4, 64)
     sd = tor.make_tube_state(0)
     if standalone:
-        net = generate_model(18, no_max_pool=True, n_classes=1039)
+        net = generate_model(18, no_max_pool=not max_pool, n_classes=1039)
         net.load_state_dict({k[len("vidnet."):]: v for k, v in sd.items() if k.startswith("vidnet.")})
         net = net.to(DEV).train()
     else:
@@ -445,14 +471,12 @@ def test_r3d_forward_standalone(standalone):
     assert logits.shape == (2, 1039)
     sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
     with torch.no_grad():
-        feat = tor.r3d18_forward(sd64, "vidnet.", video.double(), training=True)  # [b,512,t,h,w]
+        feat = tor.r3d18_forward(sd64, "vidnet.", video.double(), training=True, max_pool=max_pool)  # [b,512,t,h,w]
         ref = F.linear(feat.mean(dim=(2, 3, 4)), sd64["vidnet.fc.weight"], sd64["vidnet.fc.bias"])
     err = rel_err(logits, ref)
-    print(f"standalone={standalone}: R3D logits rel err {err:.3e}")
+    print(f"standalone={standalone} max_pool={max_pool}: R3D logits rel err {err:.3e}")
     assert err < 3e-2, err
     # train mode updated the running statistics and the batch counter, as the reference BN3d does
     bn1 = net.bn1
     assert int(bn1.num_batches_tracked) == 1
     assert not torch.equal(bn1.running_mean.cpu(), torch.zeros(64))
-    with pytest.raises(NotImplementedError):  # the stem max-pool path is not built
-        generate_model(18, no_max_pool=False).to(DEV)(video.to(DEV))
