@@ -106,7 +106,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // Timing diagnostics, compiled only into the -DAVT_DIAG build (tools/build_variant.sh; avt_build_flags()
 // reports it and bench.py refuses it): AVT_DIAG_SKIP bit mask of launches to leave out of a captured graph
 // (1: forward bn_finalize, 2: backward bn finalize, 4: wgrad slab reduce, 8: backward BN reductions, 16: forward
-// bn_apply); results are WRONG when set.  Only the captured graph leaves them out.  The persistent BN accumulators
+// bn_apply; 32 / 64: the forward / backward BN finalizes launched TWICE -- a valid marginal cost of one finalize
+// launch, every tensor keeping realistic values); results are WRONG when set.  Only the captured graph leaves them out.  The persistent BN accumulators
 // keep what the eager warm-up wrote (bits 2, 8: the replays run on realistic statistics); the tensors a skipped
 // launch would write inside the graph (bit 16) are graph-pool memory nobody wrote -- the data trap below.
 // Caveat, measured: the step's speed depends on the data -- a graph whose BN statistics are never written

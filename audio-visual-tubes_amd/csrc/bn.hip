@@ -735,8 +735,9 @@ extern "C" int avt_bn_finalize(double* acc, long long rows, int C, const float* 
   AVT_REQUIRE(rows > 0 && C > 0, "bn_finalize: empty input");
   hipStream_t st = (hipStream_t)stream;
   if (diag_skip(1, st)) return AVT_OK;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, rows, C, gamma,
-                     beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
+  for (int rep = diag_skip(32, st) ? 2 : 1; rep > 0; --rep)  // (AVT_DIAG bit 32: each launched twice, timing only)
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, rows, C,
+                       gamma, beta, running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd, 1LL);
   return check_launch("bn_finalize");
 }
 
@@ -839,6 +840,8 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   p.C = C;
   if (t2) {
     if (!diag_skip(8, st)) hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<true>, dim3(nblk), dim3(256), 0, st, a);
+    if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + kFinCB - 1) / kFinCB)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
+                       t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(2 * ((C + kFinCB - 1) / kFinCB)), dim3(kFinThreads), 0, st, acc, acc2, C, inv_rows,
                        t1->dgamma, t1->dbeta, k1, k1 + C, t2->dgamma, t2->dbeta, k1b, k1b + C);
     p.xc2 = (const bf16_t*)t2->xc;
@@ -851,6 +854,8 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<true>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
   } else {
     if (!diag_skip(8, st)) hipLaunchKernelGGL(bn_bwd_mask_reduce_kernel<false>, dim3(nblk), dim3(256), 0, st, a);
+    if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
+                       t1->dbeta, k1, k1 + C);
     if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, inv_rows, t1->dgamma,
                        t1->dbeta, k1, k1 + C);
     hipLaunchKernelGGL(bn_bwd_mask_apply_kernel<false>, dim3(ew_grid(p.nvec)), dim3(256), 0, st, p);
@@ -878,6 +883,8 @@ extern "C" int avt_bn_bwd(const void* g, const void* y, const void* xc, const fl
   if (!diag_skip(8, st))
     bn_bwd_reduce_launch((const bf16_t*)g, (const bf16_t*)y, nullptr, nullptr, (const bf16_t*)xc, mean, invstd, acc,
                          rows, C, st);
+  if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
@@ -901,6 +908,8 @@ extern "C" int avt_bn_bwd_premasked(const void* gm, const void* xc, const float*
   float* k1 = (float*)(acc + kBnHdr);
   float* k2 = k1 + C;
   hipStream_t st = (hipStream_t)stream;
+  if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
@@ -924,6 +933,8 @@ extern "C" int avt_bn_relu_bwd(const void* g, const void* xc, const float* scale
   hipStream_t st = (hipStream_t)stream;
   if (!diag_skip(8, st))
     bn_bwd_reduce_launch((const bf16_t*)g, nullptr, scale, shift, (const bf16_t*)xc, mean, invstd, acc, rows, C, st);
+  if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
+                     dgamma, dbeta, k1, k2);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C, 1.0 / (double)rows,
                      dgamma, dbeta, k1, k2);
   const long long nvec = rows * C / 8;
@@ -968,6 +979,8 @@ extern "C" int avt_stem_maxpool_bn_relu_bwd(const void* gy, const void* idx, con
   hipStream_t st = (hipStream_t)stream;
   bn_bwd_reduce_launch((const bf16_t*)gy, nullptr, scale, shift, (const bf16_t*)carg, mean, invstd, acc,
                        (long long)N * P * Q, C, st);
+  if (diag_skip(64, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C,
+                     1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   if (!diag_skip(2, st)) hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCB - 1) / kFinCB), dim3(kFinThreads), 0, st, acc, C,
                      1.0 / ((double)N * H * W), dgamma, dbeta, k1, k2);
   hipLaunchKernelGGL(stem_maxpool_bn_bwd_apply_kernel, dim3(N * ((H + 1) / 2)), dim3(kStemBwdThreads), (size_t)6 * Q * C,
