@@ -516,7 +516,10 @@ static bool halo8_pick(const GemmNTParams& p) {
   if (g_halo8 < 0) g_halo8 = getenv("AVT_HALO8") ? atoi(getenv("AVT_HALO8")) : 1;
   if (!g_halo8) return false;
   if (p.IC >= 512) return true;
-  return (long)((p.M + 255) / 256) * (p.Ng / 128) <= num_cus();
+  // (A/B, env AVT_HALO8_PCT, default 100: the grid of 256-row tiles may reach that % of the CUs -- in the step the
+  // other trunk's kernels fill a partial second round)
+  static const int pct = getenv("AVT_HALO8_PCT") ? atoi(getenv("AVT_HALO8_PCT")) : 100;
+  return (long)((p.M + 255) / 256) * (p.Ng / 128) * 100 <= (long)num_cus() * pct;
 }
 // weight-ring stages of the 8-wave 256 x 128 halo tile (A/B knob AVT_HALO8_NST: 3 default, or 4 -- the tile runs
 // one block per CU either way, so a fourth stage is one more weight tile in flight for free LDS)
