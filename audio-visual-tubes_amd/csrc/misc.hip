@@ -134,27 +134,51 @@ __global__ __launch_bounds__(256) void pack_fwd_batched_kernel(const PackDesc* _
 }
 
 // dgrad image [C][R*S][K] = transpose of w[K][R*S][C] per tap: 64x64 (k, c) tiles through LDS so
-// that both the fp32 reads (along c) and the bf16 writes (along k) are contiguous.
+// that both the fp32 reads (along c) and the bf16 writes (along k) are contiguous.  K, C multiples of 64 and 16-byte
+// aligned operands (every conv but the stems): 16-byte loads (4 c) and stores (8 k) per thread; else one element.
 __global__ __launch_bounds__(256) void pack_dgrad_batched_kernel(const PackDesc* __restrict__ descs) {
-  __shared__ float tile[64][65];
+  __shared__ __attribute__((aligned(16))) float tile[64][68];
   const PackDesc d = descs[blockIdx.y];
   if (!d.dgrad) return;
   const int kt = (d.K + 63) / 64, ct = (d.C + 63) / 64;
   const int ntiles = d.RS * kt * ct;
-  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;  // 64 x 4
+  const bool vec = (d.K % 64 == 0) && (d.C % 64 == 0) && ((((uintptr_t)d.w) | ((uintptr_t)d.dgrad)) & 15) == 0;
   for (int tile_id = blockIdx.x; tile_id < ntiles; tile_id += gridDim.x) {
     const int rs = tile_id / (kt * ct);
     const int rem = tile_id - rs * kt * ct;
     const int k0 = (rem / ct) * 64, c0 = (rem % ct) * 64;
     __syncthreads();
-    for (int i = ly; i < 64; i += 4) {  // row k0+i, column c0+lx
-      const int k = k0 + i, c = c0 + lx;
-      tile[i][lx] = (k < d.K && c < d.C) ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
-    }
-    __syncthreads();
-    for (int i = ly; i < 64; i += 4) {  // output row c0+i, column k0+lx
-      const int c = c0 + i, k = k0 + lx;
-      if (c < d.C && k < d.K) d.dgrad[((size_t)c * d.RS + rs) * d.K + k] = f2bf(tile[lx][i]);
+    if (vec) {
+      const int c4 = (threadIdx.x & 15) * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // rows k0 + (tid / 16) + 16 i, columns c0 + c4 .. +3
+        const int k = (int)(threadIdx.x >> 4) + 16 * i;
+        const float4 v = *reinterpret_cast<const float4*>(d.w + ((size_t)(k0 + k) * d.RS + rs) * d.C + c0 + c4);
+        *reinterpret_cast<float4*>(&tile[k][c4]) = v;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {  // output row c0 + q / 8, columns k0 + (q % 8) * 8 .. +7
+        const int q = (int)threadIdx.x + 256 * j;
+        const int c = q >> 3, kk = (q & 7) * 8;
+        u32x4 o;
+        o.x = pack2(tile[kk + 0][c], tile[kk + 1][c]);
+        o.y = pack2(tile[kk + 2][c], tile[kk + 3][c]);
+        o.z = pack2(tile[kk + 4][c], tile[kk + 5][c]);
+        o.w = pack2(tile[kk + 6][c], tile[kk + 7][c]);
+        *reinterpret_cast<u32x4*>(d.dgrad + ((size_t)(c0 + c) * d.RS + rs) * d.K + k0 + kk) = o;
+      }
+    } else {
+      const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;  // 64 x 4
+      for (int i = ly; i < 64; i += 4) {  // row k0+i, column c0+lx
+        const int k = k0 + i, c = c0 + lx;
+        tile[i][lx] = (k < d.K && c < d.C) ? d.w[((size_t)k * d.RS + rs) * d.C + c] : 0.f;
+      }
+      __syncthreads();
+      for (int i = ly; i < 64; i += 4) {  // output row c0+i, column k0+lx
+        const int c = c0 + i, k = k0 + lx;
+        if (c < d.C && k < d.K) d.dgrad[((size_t)c * d.RS + rs) * d.K + k] = f2bf(tile[lx][i]);
+      }
     }
   }
 }
@@ -483,7 +507,7 @@ extern "C" int avt_pack_conv_weights_batched(const void* descs, int n, long long
   AVT_REQUIRE(descs && n > 0, "pack_conv_weights_batched: bad arguments");
   AVT_REQUIRE(max_elems >= 0 && max_elems < (1ll << 31), "pack_conv_weights_batched: max_elems out of range");
   long long bx = (max_elems / 8 + 255) / 256;  // fwd: 8 elements per thread
-  if (bx > 256) bx = 256;
+  if (bx > 1024) bx = 1024;
   if (bx < 1) bx = 1;
   long long tx = max_elems / 4096 + 1;  // dgrad: 64x64 tiles
   if (tx > 512) tx = 512;
@@ -502,7 +526,7 @@ extern "C" int avt_pack_conv_weights_part(const void* descs, int n, long long ma
   AVT_REQUIRE(max_elems >= 0 && max_elems < (1ll << 31), "pack_conv_weights_part: max_elems out of range");
   if (which == 1) {
     long long bx = (max_elems / 8 + 255) / 256;
-    bx = bx > 256 ? 256 : (bx < 1 ? 1 : bx);
+    bx = bx > 1024 ? 1024 : (bx < 1 ? 1 : bx);
     hipLaunchKernelGGL(pack_fwd_batched_kernel, dim3((unsigned)bx, n), dim3(256), 0, (hipStream_t)stream,
                        (const PackDesc*)descs);
   } else {
