@@ -76,6 +76,26 @@ __global__ __launch_bounds__(256) void pack_conv3d_kernel(const float* __restric
   }
 }
 
+// fold = 0 with the filter row in LDS: out[k] is the (C x T) -> (T x C) transpose of w[k] (T = KT*R*S taps): one block
+// per output row, the fp32 row read contiguously into LDS, the bf16 row written two channels per thread (both sides
+// coalesced; the element kernel above reads with a T-float stride).  Same values as pack_conv3d_kernel.
+__global__ __launch_bounds__(256) void pack_conv3d_rows_kernel(const float* __restrict__ w, bf16_t* __restrict__ out,
+                                                               int K, int C, int T) {
+  extern __shared__ float row[];  // C * T floats
+  const int n = C * T;
+  for (int k = blockIdx.x; k < K; k += gridDim.x) {
+    const float* src = w + (size_t)k * n;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = src[i];
+    __syncthreads();
+    unsigned* dst = reinterpret_cast<unsigned*>(out + (size_t)k * n);
+    for (int j = threadIdx.x; j < n / 2; j += blockDim.x) {  // output elements 2j, 2j + 1: tap t, channels c, c + 1
+      const int t = (2 * j) / C, c = 2 * j - t * C;
+      dst[j] = pack2(row[c * T + t], row[(c + 1) * T + t]);
+    }
+  }
+}
+
 // out[(b*rep + k)][c] = in[b][c]  (the per-clip audio vector of each of its t frames)
 __global__ __launch_bounds__(256) void repeat_rows_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
                                                           int rep, int C) {
@@ -187,6 +207,13 @@ extern "C" int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, i
   AVT_REQUIRE(w && out, "pack_conv3d_weight: null pointer");
   AVT_REQUIRE(!fold || (C <= 4 && KT <= 8), "pack_conv3d_weight: stem fold needs C <= 4, KT <= 8");
   const long long total = (long long)K * (fold ? R * S * 32 : KT * R * S * C);
+  const int T = KT * R * S;
+  const size_t row_bytes = (size_t)C * T * sizeof(float);
+  if (!fold && C % 2 == 0 && row_bytes <= 60 * 1024 && ((uintptr_t)out & 3) == 0) {
+    hipLaunchKernelGGL(pack_conv3d_rows_kernel, dim3(K < 2048 ? K : 2048), dim3(256), row_bytes, (hipStream_t)stream, w,
+                       (bf16_t*)out, K, C, T);
+    return check_launch("pack_conv3d_weight");
+  }
   hipLaunchKernelGGL(pack_conv3d_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, w, (bf16_t*)out, K,
                      C, KT, R, S, fold, total);
   return check_launch("pack_conv3d_weight");

@@ -421,6 +421,20 @@ def test_hardway_attention_standalone_autograd(b, t, hw, C, normalized):
     assert rel_err(ad.grad, ar.grad) < 2e-4
 
 
+@pytest.mark.parametrize("K,C,KT,R", [(64, 64, 3, 3), (128, 64, 3, 3), (512, 256, 3, 3), (512, 512, 3, 3),
+                                        (128, 64, 1, 1), (16, 3, 3, 3), (8, 7, 3, 3)])
+def test_pack_conv3d_weight_layout(K, C, KT, R):
+    """avt_pack_conv3d_weight (fold 0): out[k][((kt*R + r)*S + s)*C + c] = bf16(w[k][c][kt][r][s]) -- the filter-row
+    transpose through LDS (even C) and the element kernel (odd C) both equal torch's permute + RNE cast, bitwise."""
+    g = torch.Generator().manual_seed(K + C + KT)
+    w = torch.randn(K, C, KT, R, R, generator=g)
+    wp = torch.empty(K, KT * R * R * C, device=DEV, dtype=torch.bfloat16)
+    wd = w.to(DEV)
+    call("avt_pack_conv3d_weight", P(wd), P(wp), K, C, KT, R, R, 0, S())
+    ref = w.permute(0, 2, 3, 4, 1).reshape(K, -1).to(torch.bfloat16)
+    assert torch.equal(wp.cpu().view(torch.int16), ref.view(torch.int16))
+
+
 @pytest.mark.parametrize("shape", [(2, 16, 112, 112, 64), (1, 5, 7, 9, 8), (3, 1, 1, 2, 16), (2, 4, 6, 6, 64)])
 def test_maxpool3d_matches_torch(shape):
     """avt_maxpool3d_fwd = nn.MaxPool3d(kernel_size=3, stride=2, padding=1) (resnet3D.py:129) on NDHWC bf16: bitwise
