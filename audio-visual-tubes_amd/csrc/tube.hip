@@ -77,21 +77,28 @@ __global__ __launch_bounds__(256) void pack_conv3d_kernel(const float* __restric
 }
 
 // fold = 0 with the filter row in LDS: out[k] is the (C x T) -> (T x C) transpose of w[k] (T = KT*R*S taps): one block
-// per output row, the fp32 row read contiguously into LDS, the bf16 row written two channels per thread (both sides
-// coalesced; the element kernel above reads with a T-float stride).  Same values as pack_conv3d_kernel.
+// per output row, the fp32 row read into LDS with 16-byte loads, the bf16 row written 8 channels (16 bytes) per
+// thread (both sides coalesced; the element kernel above reads with a T-float stride).  C % 8 == 0.  Same values as
+// pack_conv3d_kernel.
 __global__ __launch_bounds__(256) void pack_conv3d_rows_kernel(const float* __restrict__ w, bf16_t* __restrict__ out,
                                                                int K, int C, int T) {
-  extern __shared__ float row[];  // C * T floats
+  extern __shared__ __attribute__((aligned(16))) float row[];  // C * T floats
   const int n = C * T;
   for (int k = blockIdx.x; k < K; k += gridDim.x) {
-    const float* src = w + (size_t)k * n;
+    const float4* src = reinterpret_cast<const float4*>(w + (size_t)k * n);
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) row[i] = src[i];
+    for (int i = threadIdx.x; i < n / 4; i += blockDim.x) reinterpret_cast<float4*>(row)[i] = src[i];
     __syncthreads();
-    unsigned* dst = reinterpret_cast<unsigned*>(out + (size_t)k * n);
-    for (int j = threadIdx.x; j < n / 2; j += blockDim.x) {  // output elements 2j, 2j + 1: tap t, channels c, c + 1
-      const int t = (2 * j) / C, c = 2 * j - t * C;
-      dst[j] = pack2(row[c * T + t], row[(c + 1) * T + t]);
+    u32x4* dst = reinterpret_cast<u32x4*>(out + (size_t)k * n);
+    for (int j = threadIdx.x; j < n / 8; j += blockDim.x) {  // output elements 8j .. 8j + 7: tap t, channels c .. c + 7
+      const int t = (8 * j) / C, c = 8 * j - t * C;
+      const float* r0 = row + c * T + t;
+      u32x4 o;
+      o.x = pack2(r0[0], r0[T]);
+      o.y = pack2(r0[2 * T], r0[3 * T]);
+      o.z = pack2(r0[4 * T], r0[5 * T]);
+      o.w = pack2(r0[6 * T], r0[7 * T]);
+      dst[j] = o;
     }
   }
 }
@@ -209,7 +216,7 @@ extern "C" int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, i
   const long long total = (long long)K * (fold ? R * S * 32 : KT * R * S * C);
   const int T = KT * R * S;
   const size_t row_bytes = (size_t)C * T * sizeof(float);
-  if (!fold && C % 2 == 0 && row_bytes <= 60 * 1024 && ((uintptr_t)out & 3) == 0) {
+  if (!fold && C % 8 == 0 && row_bytes <= 60 * 1024 && ((((uintptr_t)out) | ((uintptr_t)w)) & 15) == 0) {
     hipLaunchKernelGGL(pack_conv3d_rows_kernel, dim3(K < 2048 ? K : 2048), dim3(256), row_bytes, (hipStream_t)stream, w,
                        (bf16_t*)out, K, C, T);
     return check_launch("pack_conv3d_weight");

@@ -422,10 +422,10 @@ def test_hardway_attention_standalone_autograd(b, t, hw, C, normalized):
 
 
 @pytest.mark.parametrize("K,C,KT,R", [(64, 64, 3, 3), (128, 64, 3, 3), (512, 256, 3, 3), (512, 512, 3, 3),
-                                        (128, 64, 1, 1), (16, 3, 3, 3), (8, 7, 3, 3)])
+                                        (128, 64, 1, 1), (16, 3, 3, 3), (8, 7, 3, 3), (32, 12, 3, 3)])
 def test_pack_conv3d_weight_layout(K, C, KT, R):
     """avt_pack_conv3d_weight (fold 0): out[k][((kt*R + r)*S + s)*C + c] = bf16(w[k][c][kt][r][s]) -- the filter-row
-    transpose through LDS (even C) and the element kernel (odd C) both equal torch's permute + RNE cast, bitwise."""
+    transpose through LDS (C % 8 == 0) and the element kernel (other C) both equal torch's permute + RNE cast, bitwise."""
     g = torch.Generator().manual_seed(K + C + KT)
     w = torch.randn(K, C, KT, R, R, generator=g)
     wp = torch.empty(K, KT * R * R * C, device=DEV, dtype=torch.bfloat16)
