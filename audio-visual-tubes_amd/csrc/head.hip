@@ -115,11 +115,8 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
                                                     long long sbn, const float* __restrict__ rowscale,
                                                     const float* __restrict__ kscale, float* __restrict__ c,
                                                     long long ldc, int k_per_split, int accum) {
-  // two LDS buffers: a k-tile is stashed into one while the other's reads may still be in flight, so one barrier
-  // per k-tile (the next stash into a buffer comes a full barrier after its last read)
-  __shared__ __attribute__((aligned(16))) float As2[2][kSgKT][64 + 4];
-  __shared__ __attribute__((aligned(16))) float Bs2[2][kSgKT][64 + 4];
-  int buf = 0;
+  __shared__ __attribute__((aligned(16))) float As[kSgKT][64 + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[kSgKT][64 + 4];
   const int tid = threadIdx.x;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int kbeg = blockIdx.z * k_per_split, kend = min(K, kbeg + k_per_split);
@@ -159,8 +156,6 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
     }
   };
   auto stash = [&]() {
-    float(*As)[64 + 4] = As2[buf];
-    float(*Bs)[64 + 4] = Bs2[buf];
     if (a_kf) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) As[a_k + e][a_r] = ra[e];
@@ -184,15 +179,13 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int N, int K, const T
     stash();
     __syncthreads();
     if (k0 + kSgKT < kend) fetch(k0 + kSgKT);  // in flight during this tile's MFMAs
-    const float(*As)[64 + 4] = As2[buf];
-    const float(*Bs)[64 + 4] = Bs2[buf];
 #pragma unroll
     for (int kp = 0; kp < kSgKT; kp += 2) {
       const float av = As[kp + fk][wm * 32 + frow];
       const float bv = Bs[kp + fk][wn * 32 + frow];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
     }
-    buf ^= 1;
+    __syncthreads();
   }
   // C layout of a 32x32 MFMA tile: element v of lane l is row (v&3) + 8(v>>2) + 4(l>>5), column l&31
   const int gn = n0 + wn * 32 + frow;
