@@ -224,3 +224,48 @@ def test_side_stream_adam_ordering_without_host_sync(monkeypatch):
         torch.cuda.synchronize()
         assert torch.equal(snap, ref_m._flat.flat), f"step {i}: weights read before the side-stream Adam finished"
     assert step._seg_graphs is not None and len(step._seg_graphs) == 2
+
+
+def test_dp_mean_gradient_vs_oracle():
+    """VERDICT r5 weak 7 (multi-GPU pinned only through self-consistency): the data-parallel gradient -- the mean over
+    ranks of each rank's local-negative gradient (nn.DataParallel semantics: the head per replica, model.py:114-115;
+    train_hardway_1frame.py:93) -- against the fp64 oracle directly.  The HIP gradient is the two shards' mean, which
+    the two-rank all-reduce reproduces bit for bit (test_two_rank_allreduce_matches_dp_mean); the oracle's is the mean
+    of orc.train_step's per-shard fp64 gradients.  The full-batch gradient (negatives from all four clips -- what a
+    global-negative mode would compute, not the reference) is a different vector, and the HIP one must sit near the
+    shard mean, not near it.  Bound: SURVEY 8(c)'s 5e-2 relative, on the whole gradient vector."""
+    import avtubes  # noqa: F401
+
+    dev = torch.device("cuda", 0)
+    m = _model(dev)
+    shards = _shards()
+    for img, aud in shards:
+        _, logits, _, _, _ = m(img.to(dev), aud.to(dev))
+        loss = torch.nn.CrossEntropyLoss()(logits, torch.zeros(logits.shape[0], dtype=torch.long, device=dev))
+        (loss / len(shards)).backward()
+    torch.cuda.synchronize()
+    names = orc.trainable_names(orc.make_state(0))
+    params = dict(m.named_parameters())
+
+    def oracle_grads(batches):
+        acc = None
+        for img, aud in batches:
+            sd = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in orc.make_state(0).items()}
+            _, _, g = orc.train_step(sd, img.double(), aud.double())
+            acc = g if acc is None else {n: acc[n] + g[n] for n in names}
+        return {n: acc[n] / len(batches) for n in names}
+
+    g_dp = oracle_grads(shards)
+    full = (torch.cat([s[0] for s in shards]), torch.cat([s[1] for s in shards]))
+    g_full = oracle_grads([full])
+    hip = torch.cat([params[n].grad.detach().double().cpu().flatten() for n in names])
+    ref = torch.cat([g_dp[n].flatten() for n in names])
+    alt = torch.cat([g_full[n].flatten() for n in names])
+    err = ((hip - ref).norm() / ref.norm()).item()
+    err_full = ((hip - alt).norm() / alt.norm()).item()
+    sep = ((alt - ref).norm() / ref.norm()).item()
+    cos = torch.nn.functional.cosine_similarity(hip, ref, dim=0).item()
+    print(f"DP-mean gradient vs fp64 oracle: rel {err:.3e}, cos {cos:.5f}; vs the full-batch gradient: rel {err_full:.3e} "
+          f"(full-batch vs shard mean: {sep:.3e})")
+    assert err <= 5e-2 and cos >= 0.995, (err, cos)
+    assert err_full > 2 * err, (err, err_full)
