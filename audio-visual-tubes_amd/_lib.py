@@ -101,6 +101,8 @@ SIGNATURES = {
     "avt_conv3d_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_video_stem_im2col": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "avt_maxpool3d_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P]),
+    "avt_pack3d_desc_bytes": (_Z, []),
+    "avt_pack_conv3d_weights_batched": (_I, [_P, _I, _I, _I, _P]),
     "avt_pack_conv3d_weight": (_I, [_P, _P, _I, _I, _I, _I, _I, _I, _P]),
     "avt_repeat_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),
     "avt_sum_rep_rows_f32": (_I, [_P, _P, _I, _I, _I, _P]),

@@ -103,6 +103,46 @@ __global__ __launch_bounds__(256) void pack_conv3d_rows_kernel(const float* __re
   }
 }
 
+// Every non-stem Conv3d weight of the R3D trunk in ONE launch (blockIdx.y = conv): the filter-row transpose above per
+// descriptor, its element form for a descriptor the 16-byte path cannot take (C % 8 != 0 or misaligned operands).
+struct Pack3dDesc {
+  const float* w;  // fp32 OIDHW [K][C][T]
+  bf16_t* out;     // bf16 [K][T*C]
+  int K, C, T, pad_;
+};
+
+__global__ __launch_bounds__(256) void pack_conv3d_batched_kernel(const Pack3dDesc* __restrict__ descs) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  const Pack3dDesc d = descs[blockIdx.y];
+  const int n = d.C * d.T;
+  const bool vec = d.C % 8 == 0 && ((((uintptr_t)d.w) | ((uintptr_t)d.out)) & 15) == 0;
+  for (int k = blockIdx.x; k < d.K; k += gridDim.x) {
+    const float* wk = d.w + (size_t)k * n;
+    bf16_t* ok = d.out + (size_t)k * n;
+    if (!vec) {
+      for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const int t = j / d.C, c = j - t * d.C;
+        ok[j] = f2bf(wk[c * d.T + t]);
+      }
+      continue;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
+      reinterpret_cast<float4*>(row)[i] = reinterpret_cast<const float4*>(wk)[i];
+    __syncthreads();
+    for (int j = threadIdx.x; j < n / 8; j += blockDim.x) {
+      const int t = (8 * j) / d.C, c = 8 * j - t * d.C;
+      const float* r0 = row + c * d.T + t;
+      u32x4 o;
+      o.x = pack2(r0[0], r0[d.T]);
+      o.y = pack2(r0[2 * d.T], r0[3 * d.T]);
+      o.z = pack2(r0[4 * d.T], r0[5 * d.T]);
+      o.w = pack2(r0[6 * d.T], r0[7 * d.T]);
+      reinterpret_cast<u32x4*>(ok)[j] = o;
+    }
+  }
+}
+
 // out[(b*rep + k)][c] = in[b][c]  (the per-clip audio vector of each of its t frames)
 __global__ __launch_bounds__(256) void repeat_rows_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
                                                           int rep, int C) {
@@ -237,6 +277,19 @@ extern "C" int avt_maxpool3d_fwd(const void* x, void* y, int N, int T, int H, in
   hipLaunchKernelGGL(maxpool3d_k3s2p1_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                      (bf16_t*)y, N, T, H, W, C, To, Ho, Wo);
   return check_launch("maxpool3d_fwd");
+}
+
+extern "C" size_t avt_pack3d_desc_bytes(void) { return sizeof(Pack3dDesc); }
+
+// descs: device array of n records {const float* w; void* out; int K, C, T, pad} (avt_pack3d_desc_bytes() each):
+// out[k][t*C + c] = bf16(w[k][c][t]) for every record in one launch; max_k = the largest K, max_row = the largest
+// C*T (floats; <= 15360: one fp32 filter row in LDS)
+extern "C" int avt_pack_conv3d_weights_batched(const void* descs, int n, int max_k, int max_row, void* stream) {
+  AVT_REQUIRE(descs && n > 0 && max_k > 0, "pack_conv3d_weights_batched: bad arguments");
+  AVT_REQUIRE(max_row > 0 && max_row <= 15360, "pack_conv3d_weights_batched: max_row=%d (<= 15360 floats)", max_row);
+  hipLaunchKernelGGL(pack_conv3d_batched_kernel, dim3(max_k < 512 ? max_k : 512, n), dim3(256),
+                     (size_t)max_row * sizeof(float), (hipStream_t)stream, (const Pack3dDesc*)descs);
+  return check_launch("pack_conv3d_weights_batched");
 }
 
 // Audio de-duplication of the tube step (train_3D.py:128-130 repeats each clip's spectrogram t

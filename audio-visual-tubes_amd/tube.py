@@ -168,6 +168,34 @@ class R3DTrunk:
         return h
 
 
+def _alloc_packs3d(engine, dev):
+    """bf16 fwd operands of the R3D convs and the device table of the non-stem ones (one batched pack launch)."""
+    import struct
+
+    descs, max_k, max_row = [], 1, 1
+    for spec in engine.vid.convs():
+        wp = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+        engine.packs3d[spec.name] = wp
+        if not spec.stem:
+            t = spec.kt * spec.k * spec.k
+            descs.append(struct.pack("<QQiiii", engine.flat.raw(spec.name).data_ptr(), wp.data_ptr(), spec.cout,
+                                     spec.cin, t, 0))
+            max_k, max_row = max(max_k, spec.cout), max(max_row, spec.cin * t)
+    assert descs and len(descs[0]) == int(query("avt_pack3d_desc_bytes"))
+    engine._pack3d_table = torch.frombuffer(bytearray(b"".join(descs)), dtype=torch.uint8).to(dev)
+    engine._pack3d_n, engine._pack3d_max = len(descs), (max_k, max_row)
+
+
+def _pack3d(engine):
+    """vidnet weights (fp32 OIDHW, never updated by the optimizer) -> bf16 fwd operands, repacked every step so a
+    load_state_dict is always picked up: the folded stem (its own layout) and one launch for the other 19 convs."""
+    stem = engine.vid.stem
+    call("avt_pack_conv3d_weight", P(engine.flat.raw(stem.name)), P(engine.packs3d[stem.name]), stem.cout, stem.cin,
+         stem.kt, stem.k, stem.k, 1, stream_ptr())
+    call("avt_pack_conv3d_weights_batched", P(engine._pack3d_table), engine._pack3d_n, *engine._pack3d_max,
+         stream_ptr())
+
+
 class _TubeStore(_EngineStore):
     def packed3d(self, spec: Conv3dSpec):
         return self.e.packs3d[spec.name]
@@ -189,17 +217,11 @@ class TubeEngine(AVEngine):
 
     def _alloc(self, dev):
         super()._alloc(dev)
-        for spec in self.vid.convs():
-            self.packs3d[spec.name] = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+        _alloc_packs3d(self, dev)
 
     def pack_weights(self):
         super().pack_weights()
-        # vidnet weights (fp32 OIDHW, never updated by the optimizer) -> bf16 fwd operands.  Repacked
-        # every step (33 M params, ~40 us) so a load_state_dict is always picked up.
-        for spec in self.vid.convs():
-            w = self.flat.raw(spec.name)
-            call("avt_pack_conv3d_weight", P(w), P(self.packs3d[spec.name]), spec.cout, spec.cin, spec.kt, spec.k,
-                 spec.k, int(spec.stem), stream_ptr())
+        _pack3d(self)
 
     # ----------------------------------------------------------------------------- forward
     def forward(self, audio: torch.Tensor, video: torch.Tensor, training: bool, with_ce: bool = False,
@@ -305,7 +327,7 @@ class TubeEngine(AVEngine):
 
 class R3DEngine(AVEngine):
     """The R3D-18 trunk called on its own -- ``FullModel.vidnet(video)`` or a standalone
-    ``resnet3D.generate_model(18, no_max_pool=True, ...)(video)`` (resnet3D.py:197-213): the conv stem ..
+    ``resnet3D.generate_model(18, ...)(video)`` (resnet3D.py:197-213; with or without the stem max-pool): the conv stem ..
     layer4 on libavt as inside FullModel (R3DTrunk), then AdaptiveAvgPool3d((1,1,1)) + fc on the pooled
     fp32 features.  Forward only, as everywhere in this build (FullModel detaches the video trunk)."""
 
@@ -326,13 +348,10 @@ class R3DEngine(AVEngine):
 
     def _alloc(self, dev):
         super()._alloc(dev)
-        for spec in self.vid.convs():
-            self.packs3d[spec.name] = torch.empty(spec.cout, spec.kg, device=dev, dtype=torch.bfloat16)
+        _alloc_packs3d(self, dev)
 
     def pack_weights(self):
-        for spec in self.vid.convs():
-            call("avt_pack_conv3d_weight", P(self.flat.raw(spec.name)), P(self.packs3d[spec.name]), spec.cout,
-                 spec.cin, spec.kt, spec.k, spec.k, int(spec.stem), stream_ptr())
+        _pack3d(self)
 
     def forward(self, video: torch.Tensor, training: bool) -> torch.Tensor:
         """video fp32 [b,3,t,H,W] -> fc logits [b, n_classes] fp32."""

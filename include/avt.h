@@ -29,7 +29,8 @@
  *   avt_conv3d_fwd               nn.Conv3d fwd of the R3D-18 video trunk (models/resnet3D.py:14-28 conv3x3x3 /
  *                                conv1x1x1, called from BasicBlock.forward 45-61; FullModel.vidnet, model.py:20)
  *   avt_video_stem_im2col,       the R3D stem Conv3d(3,64,(7,7,7),s(1,2,2),p3) (models/resnet3D.py:122-127) as a
- *   avt_pack_conv3d_weight       32-channel Conv2d over the frames (temporal taps folded into channels)
+ *   avt_pack_conv3d_weight       32-channel Conv2d over the frames (temporal taps folded into channels);
+ *   (+ _weights_batched)         the other Conv3d weights' bf16 operands in one launch
  *   avt_maxpool3d_fwd            the R3D stem's nn.MaxPool3d(3, 2, 1) when no_max_pool=False (resnet3D.py:129, 200-201)
  *   avt_bn_finalize_rep          BatchNorm2d over the t-fold repeated spectrogram batch (train_3D.py:128-130)
  *                                computed once per distinct clip
@@ -184,6 +185,11 @@ int avt_video_stem_im2col(const float* x, void* out, int N, int C, int T, int H,
 /* w fp32 OIDHW [K][C][KT][R][S] -> bf16 [K][(kt,r,s,c)] (fold 0) or the stem layout
  * [K][(r,s)][kt*4+c] with 32 channels per (r,s) (fold 1) */
 int avt_pack_conv3d_weight(const float* w, void* out, int K, int C, int KT, int R, int S, int fold, void* stream);
+/* every non-stem Conv3d weight in one launch: descs = device array of n records {const float* w; void* out; int K,
+ * C, T, pad} (avt_pack3d_desc_bytes() bytes each), out[k][t*C + c] = bf16(w[k][c][t]) (T = KT*R*S, the fold-0 layout
+ * of avt_pack_conv3d_weight); max_k = the largest K, max_row = the largest C*T (<= 15360) */
+size_t avt_pack3d_desc_bytes(void);
+int avt_pack_conv3d_weights_batched(const void* descs, int n, int max_k, int max_row, void* stream);
 /* nn.MaxPool3d(kernel_size=3, stride=2, padding=1) over bf16 NDHWC [N][T][H][W][C], C % 8 == 0 ->
  * [N][(T-1)/2+1][(H-1)/2+1][(W-1)/2+1][C] (the winning input's bits; NaN propagates) */
 int avt_maxpool3d_fwd(const void* x, void* y, int N, int T, int H, int W, int C, void* stream);

@@ -435,6 +435,38 @@ def test_pack_conv3d_weight_layout(K, C, KT, R):
     assert torch.equal(wp.cpu().view(torch.int16), ref.view(torch.int16))
 
 
+def test_pack_conv3d_weights_batched_matches_single():
+    """avt_pack_conv3d_weights_batched (one launch for every non-stem R3D conv) == avt_pack_conv3d_weight per conv,
+    bitwise: 16-byte filter-row path, and the element path for C % 8 != 0 and for a misaligned source."""
+    import struct
+
+    # K, C, T, flat offset (floats)
+    cases = [(64, 64, 27, 0), (128, 64, 1, 110592), (512, 512, 27, 118784), (16, 12, 27, 7196672),
+             (8, 7, 9, 7201856), (32, 16, 27, 7202363)]
+    total = max(o + K * C * T for K, C, T, o in cases)
+    g = torch.Generator().manual_seed(9)
+    flat = torch.randn(total, generator=g).to(DEV)
+    descs, outs, singles = [], [], []
+    for K, C, T, o in cases:
+        w = flat[o:o + K * C * T]
+        out = torch.empty(K, C * T, device=DEV, dtype=torch.bfloat16)
+        descs.append(struct.pack("<QQiiii", w.data_ptr(), out.data_ptr(), K, C, T, 0))
+        outs.append(out)
+        one = torch.empty_like(out)
+        kt, r = (3, 3) if T == 27 else (1, 3) if T == 9 else (1, 1)
+        call("avt_pack_conv3d_weight", P(w), P(one), K, C, kt, r, r, 0, S())
+        singles.append(one)
+    assert len(descs[0]) == int(query("avt_pack3d_desc_bytes"))
+    table = torch.frombuffer(bytearray(b"".join(descs)), dtype=torch.uint8).to(DEV)
+    call("avt_pack_conv3d_weights_batched", P(table), len(descs), max(c[0] for c in cases),
+         max(c[1] * c[2] for c in cases), S())
+    torch.cuda.synchronize()
+    for out, one in zip(outs, singles):
+        assert torch.equal(out.view(torch.int16), one.view(torch.int16))
+    with pytest.raises(RuntimeError):
+        call("avt_pack_conv3d_weights_batched", P(table), len(descs), 512, 15361, S())
+
+
 @pytest.mark.parametrize("shape", [(2, 16, 112, 112, 64), (1, 5, 7, 9, 8), (3, 1, 1, 2, 16), (2, 4, 6, 6, 64)])
 def test_maxpool3d_matches_torch(shape):
     """avt_maxpool3d_fwd = nn.MaxPool3d(kernel_size=3, stride=2, padding=1) (resnet3D.py:129) on NDHWC bf16: bitwise
