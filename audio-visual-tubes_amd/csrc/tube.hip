@@ -47,53 +47,6 @@ __global__ __launch_bounds__(256) void video_stem_im2col_kernel(const float* __r
   }
 }
 
-// Two horizontally adjacent output pixels per thread (H*W even, x 8-byte aligned): 8-byte loads, the same values.
-__global__ __launch_bounds__(256) void video_stem_im2col2_kernel(const float* __restrict__ x, bf16_t* __restrict__ out,
-                                                                 int N, int C, int T, int HW, int KT, int pad_t) {
-  const long long npair = (long long)N * T * (HW / 2);
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npair;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long pix = 2 * i;
-    const int hw = (int)(pix % HW);
-    const long long nt = pix / HW;
-    const int t = (int)(nt % T), n = (int)(nt / T);
-    float v0[32], v1[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      v0[j] = 0.f;
-      v1[j] = 0.f;
-    }
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      if (kt >= KT) break;
-      const int tt = t + kt - pad_t;
-      if (tt < 0 || tt >= T) continue;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c < C) {
-          const float2 f = *reinterpret_cast<const float2*>(x + (((long long)n * C + c) * T + tt) * HW + hw);
-          v0[kt * 4 + c] = f.x;
-          v1[kt * 4 + c] = f.y;
-        }
-    }
-    u32x4* o = reinterpret_cast<u32x4*>(out + pix * 32);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      u32x4 a, b;
-      a[0] = pack2(v0[q * 8 + 0], v0[q * 8 + 1]);
-      a[1] = pack2(v0[q * 8 + 2], v0[q * 8 + 3]);
-      a[2] = pack2(v0[q * 8 + 4], v0[q * 8 + 5]);
-      a[3] = pack2(v0[q * 8 + 6], v0[q * 8 + 7]);
-      b[0] = pack2(v1[q * 8 + 0], v1[q * 8 + 1]);
-      b[1] = pack2(v1[q * 8 + 2], v1[q * 8 + 3]);
-      b[2] = pack2(v1[q * 8 + 4], v1[q * 8 + 5]);
-      b[3] = pack2(v1[q * 8 + 6], v1[q * 8 + 7]);
-      o[q] = a;
-      o[4 + q] = b;
-    }
-  }
-}
-
 // fold = 0: out[k][((kt*R + r)*S + s)*C + c] = w[k][c][kt][r][s]            (Kg = KT*R*S*C)
 // fold = 1: out[k][(r*S + s)*32 + kt*4 + c] = w[k][c][kt][r][s], zero padded (Kg = R*S*32)
 __global__ __launch_bounds__(256) void pack_conv3d_kernel(const float* __restrict__ w, bf16_t* __restrict__ out, int K,
@@ -290,11 +243,6 @@ extern "C" int avt_video_stem_im2col(const float* x, void* out, int N, int C, in
   AVT_REQUIRE(C >= 1 && C <= 4 && KT >= 1 && KT <= 7, "video_stem_im2col: need C <= 4 and KT <= 7");
   const long long npix = (long long)N * T * H * W;
   if (npix == 0) return AVT_OK;
-  if ((H * W) % 2 == 0 && ((uintptr_t)x & 7) == 0) {
-    hipLaunchKernelGGL(video_stem_im2col2_kernel, dim3(grid_for(npix / 2)), dim3(256), 0, (hipStream_t)stream, x,
-                       (bf16_t*)out, N, C, T, H * W, KT, pad_t);
-    return check_launch("video_stem_im2col");
-  }
   hipLaunchKernelGGL(video_stem_im2col_kernel, dim3(grid_for(npix)), dim3(256), 0, (hipStream_t)stream, x,
                      (bf16_t*)out, N, C, T, H * W, KT, pad_t);
   return check_launch("video_stem_im2col");
