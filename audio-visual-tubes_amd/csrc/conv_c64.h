@@ -265,29 +265,14 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
     }
     // bf16 pairs: lanes 2k / 2k+1 hold columns c / c+1 of the same rows; per pair of accumulator
     // values (v, v+1) = rows (r, r+1) the even lane stores row r (c, c+1), the odd lane row r+1 (c-1, c).
-    // The tile's `add` words (and mask bytes) -- all TM x 2 accumulators' -- are loaded together before any is
-    // used: one memory round trip per tile.
+    // Per 32x32 accumulator the 8 `add` words (and mask bytes) are loaded together before any is used.
     const bool odd = lane & 1;
-    unsigned av[TM][2][8], mv[TM][2][8];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if constexpr (ADD != 0) {
-            const int v = 2 * u;
-            const int r = wid * WR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf + (odd ? 1 : 0);
-            const size_t off = (size_t)(m0 + (r < rows_valid ? r : 0)) * 64 + j * 32 + (frow & ~1);
-            av[i][j][u] = *reinterpret_cast<const unsigned*>(p.add + off);
-            if (ADD == 2) mv[i][j][u] = p.amask[off >> 3];
-          }
-        }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = j * 32 + (frow & ~1);
+        unsigned av[8], mv[8];
         size_t offs[8];
         bool okv[8];
 #pragma unroll
@@ -296,6 +281,8 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
           const int r = wid * WR + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fhalf + (odd ? 1 : 0);
           okv[u] = r < rows_valid;
           offs[u] = (size_t)(m0 + (okv[u] ? r : 0)) * 64 + c;  // element offset of the pair
+          if (ADD) av[u] = *reinterpret_cast<const unsigned*>(p.add + offs[u]);
+          if (ADD == 2) mv[u] = p.amask[offs[u] >> 3];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -303,9 +290,9 @@ __global__ __launch_bounds__(NWAVE * 64, 1) void conv_c64_kernel(GemmNTParams p,
           const float r0 = c64_swap1(a0), r1 = c64_swap1(a1);
           unsigned o = odd ? pack2(r1, a1) : pack2(a0, r0);
           if (ADD) {
-            unsigned a = av[i][j][u];
+            unsigned a = av[u];
             if (ADD == 2) {
-              const unsigned bits = mv[i][j][u] >> (c & 7);
+              const unsigned bits = mv[u] >> (c & 7);
               a &= (bits & 1u ? 0x0000ffffu : 0u) | (bits & 2u ? 0xffff0000u : 0u);
             }
             o = pack2(bf2f(o & 0xffff) + bf2f(a & 0xffff), bf2f(o >> 16) + bf2f(a >> 16));
