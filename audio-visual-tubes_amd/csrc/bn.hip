@@ -707,23 +707,14 @@ __global__ __launch_bounds__(kStemBwdThreads) void stem_maxpool_bn_bwd_apply_ker
   }
 }
 
-// rows per block of the BN backward reductions: ~AVT_BN_RED_BLOCKS blocks (A/B knob, default 512: two per CU) in
-// whole row steps, at most the accumulator's slot capacity
-static long long bn_red_rows_per_block(long long rows, int C) {
-  static const long long target = getenv("AVT_BN_RED_BLOCKS") ? atoll(getenv("AVT_BN_RED_BLOCKS")) : 512;
-  const int rstep = 256 / (C / 8);
-  long long rpb = (rows + target - 1) / target;
-  const long long cap = bn_slot_cap(rows);
-  if ((rows + rpb - 1) / rpb > cap) rpb = (rows + cap - 1) / cap;
-  rpb = ((rpb + rstep - 1) / rstep) * rstep;
-  if (rpb < rstep) rpb = rstep;
-  return rpb;
-}
-
 static void bn_bwd_reduce_launch(const bf16_t* g, const bf16_t* y, const float* mscale, const float* mshift,
                                  const bf16_t* xc, const float* mean, const float* invstd, double* acc, long long rows,
                                  int C, hipStream_t st) {
-  const long long rpb = bn_red_rows_per_block(rows, C);
+  // ~2 blocks per CU of rows (more blocks measured slower: their fp64 atomics contend)
+  long long rpb = (rows + 511) / 512;
+  const int rstep = 256 / (C / 8);
+  rpb = ((rpb + rstep - 1) / rstep) * rstep;
+  if (rpb < rstep) rpb = rstep;
   const int nblk = (int)((rows + rpb - 1) / rpb);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(256), 0, st, g, y, mscale, mshift, xc, mean, invstd, acc,
                      rows, C, (int)rpb);
@@ -828,7 +819,10 @@ extern "C" int avt_bn_bwd_mask(const void* g, const void* mask, const avt_bn_bwd
   }
   a.rows = rows;
   a.C = C;
-  const long long rpb = bn_red_rows_per_block(rows, C);  // as bn_bwd_reduce_launch
+  long long rpb = (rows + 511) / 512;  // ~2 blocks per CU of rows, as bn_bwd_reduce_launch
+  const int rstep = 256 / (C / 8);
+  rpb = ((rpb + rstep - 1) / rstep) * rstep;
+  if (rpb < rstep) rpb = rstep;
   a.rows_per_block = (int)rpb;
   const int nblk = (int)((rows + rpb - 1) / rpb);
   const double inv_rows = 1.0 / (double)rows;
