@@ -558,8 +558,7 @@ class AVEngine:
         return gv, gan
 
     def backward(self, tape, dlogits: Optional[torch.Tensor], gflat: torch.Tensor, on_boundary=None,
-                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None, on_trunk_end=None,
-                 on_trunk_hi=None):
+                 dwA: Optional[torch.Tensor] = None, dA=None, dPos=None, dNeg=None, on_trunk_end=None):
         """Accumulate d(loss)/d(params) into gflat[:n_train] (caller zeroes it).
         dwA: upstream gradient of weighted_A (the 16-frame losses, train_hardway.py:138-141); dA/dPos/dNeg:
         of the returned maps.  The two trunks' backward runs concurrently (audio on the side stream) in
@@ -569,8 +568,7 @@ class AVEngine:
         there sees those buckets final (train.py overlaps them with the second segment).
         on_trunk_end(trunk) (without on_boundary): called on each trunk's stream behind its last gradient
         launch -- that trunk's gradients are final there (train.py updates them while the other trunk's
-        backward still runs).  on_trunk_hi(trunk) (likewise): on the trunk's stream once its layer4+layer3
-        gradients (the "hi" bucket) are final, before its layer2..stem backward."""
+        backward still runs)."""
         gv, gan = self.head_backward(tape, dlogits, dwA, dA=dA, dPos=dPos, dNeg=dNeg)
         a = tape["a"]
         B, C = tape["B"], tape["C"]
@@ -599,8 +597,6 @@ class AVEngine:
 
         def chain(tr, tp, first):
             g, pm = yield from first
-            if on_trunk_hi is not None:
-                on_trunk_hi(tr)
             yield from lo(tr, tp, g, pm)
             if on_trunk_end is not None:  # on the trunk's stream, behind its last gradient launch
                 on_trunk_end(tr)

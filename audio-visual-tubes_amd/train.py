@@ -79,9 +79,6 @@ class HardWayTrainStep:
                             and type(self.engine).backward is AVEngine.backward)
         # Adam's step counter and the gradient zeroing on the vision branch (AVT_VISION_PRE=0: serial)
         self.vision_pre = os.environ.get("AVT_VISION_PRE", "1") != "0"
-        # with adam_branch: each trunk's layer4+layer3 parameters ("hi" bucket) updated on a side stream as soon as
-        # their gradients are final, beside that trunk's layer2..stem backward (AVT_ADAM_HI=1; A/B knob)
-        self.adam_hi = self.adam_branch and os.environ.get("AVT_ADAM_HI", "0") != "0"
 
     def _fwd_bwd(self, *inputs, on_boundary=None) -> torch.Tensor:
         image, audio = inputs
@@ -109,28 +106,17 @@ class HardWayTrainStep:
             self.grad.zero_()
         done = []
 
-        def trunk_hi(tr):  # on the trunk's stream: its "hi" gradients are final
-            lo, hi = self.buckets[tr.prefix + "hi"]
-            side = self._adam_stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                self.opt.apply(self.grad, lo, hi)
-            done.append((lo, hi))
-
         def trunk_end(tr):
-            lo, hi = self.buckets[tr.prefix + "lo"] if self.adam_hi else self._trunk_region(tr)
+            lo, hi = self._trunk_region(tr)
             self.opt.apply(self.grad, lo, hi)
             done.append((lo, hi))
 
-        self.engine.backward(tape, out["dlogits"], self.grad, None, on_trunk_end=trunk_end,
-                             on_trunk_hi=trunk_hi if self.adam_hi else None)
+        self.engine.backward(tape, out["dlogits"], self.grad, None, on_trunk_end=trunk_end)
         pos = 0
         for lo, hi in sorted(done) + [(self.flat.n_train, self.flat.n_train)]:
             if lo > pos:
                 self.opt.apply(self.grad, pos, lo)
             pos = max(pos, hi)
-        if self.adam_hi:
-            torch.cuda.current_stream().wait_stream(self._adam_stream())
         return out["loss"]
 
     def step(self, *inputs: torch.Tensor) -> torch.Tensor:
